@@ -1,0 +1,242 @@
+"""Benchmark: aggregate agent-steps/s of the device-resident greedy rollout (BASELINE.json config 3).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Workload (per GPU, weak scaling): WarehouseMedium, 8 agents, B = 65,536 envs, greedy policy
+(baseline/solvers.py:27-58) fused with Warehouse.step() (warehouse/core.py:262-442) and
+auto-reset, philox draws keyed by global env id (rank r owns ids [r*B, (r+1)*B)).  One "step" = one
+policy+transition for every env; every step writes rewards [B,8] f32 and dones [B] u8.  Ranks share
+nothing on the data path (no RCCL); a gloo group only aligns the timing window and takes the max.
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  roofline     -- algorithmic bytes of the step kernel / its mean duration (HIP events on the
+                  launch stream), against the 8 TB/s HBM peak; `traffic` from the committed
+                  rocprofv3 PMC summary (profiles/) when present.
+  cpu_baseline -- the numpy restatement of warehouse.core.Warehouse.step() (oracle/core.py), one
+                  env per process, step-only timing, on a bounded sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "rllib-warehouse_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "agent-steps/sec (aggregate) at B=65536 envs × 8 agents, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
+
+
+def cpu_worker(args):
+    """One process = one env (oracle restatement of warehouse.core.Warehouse.step()); returns
+    (agent-steps, seconds spent inside step())."""
+    variant, n, seconds, seed = args
+    import numpy as np
+
+    from oracle import core as oc
+
+    np.random.seed(seed)
+    env = oc.OracleWarehouse(variant, n)
+    obs = env.reset()
+    draws = env.draws
+    steps, spent = 0, 0.0
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        flat = np.stack([np.concatenate([np.asarray(obs[str(i)][k]).ravel() for k in oc.OBS_KEYS])
+                         for i in range(n)])
+        acts = oc.greedy(env.layout, flat, 0.0, draws)
+        ad = {str(i): int(acts[i]) for i in range(n)}
+        t0 = time.perf_counter()
+        obs, _, dones, _ = env.step(ad)
+        spent += time.perf_counter() - t0
+        steps += 1
+        if dones["__all__"]:
+            obs = env.reset()
+    return steps * n, spent
+
+
+def cpu_baseline(variant, n, procs, seconds):
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(cpu_worker, [(variant, n, seconds, 1000 + i) for i in range(procs)])
+    rate = sum(a / s for a, s in res if s > 0)
+    return dict(value=rate, unit="agent-steps/s", cores=procs, kind="port",
+                sample=f"{procs} processes x {seconds:.1f} s, 1 env each, {variant} N={n}, greedy actions, "
+                       f"step-only time of oracle/core.py OracleWarehouse.step (numpy restatement of "
+                       f"warehouse.core.Warehouse.step)")
+
+
+def load_traffic(tag):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get(tag, {}).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--variant", default="medium")
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--policy", default="greedy", choices=["greedy", "random"])
+    ap.add_argument("--mode", default="graph", choices=["graph", "fused"],
+                    help="graph: hipGraph of one-step launches (state round-trips HBM every step); "
+                         "fused: --chunk steps per launch, state in registers")
+    ap.add_argument("--chunk", type=int, default=200)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import warehouse
+
+    B, NA, K, W = args.envs, args.agents, args.steps, args.warmup
+    env = warehouse.BatchedWarehouse(args.variant, B, NA, seed=1234, env_offset=rank * B, device=dev)
+    env.reset()
+    words = env.layout.words_per_env
+    stream = torch.cuda.current_stream(dev)
+
+    if args.mode == "graph":
+        rew = torch.zeros((1, B, NA), device=dev)
+        dn = torch.zeros((1, B), dtype=torch.uint8, device=dev)
+
+        def one():
+            env.rollout(1, args.policy, 0.0, rewards=rew, dones=dn)
+
+        for _ in range(max(W, 3)):
+            one()
+        torch.cuda.synchronize(dev)
+        G = min(K, 200)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(G):
+                one()
+        torch.cuda.synchronize(dev)
+
+        def run_steps(k):
+            for _ in range(k // G):
+                graph.replay()
+            for _ in range(k % G):
+                one()
+        per_launch_steps = 1
+    else:
+        C = args.chunk
+        rew = torch.zeros((C, B, NA), device=dev)
+        dn = torch.zeros((C, B), dtype=torch.uint8, device=dev)
+
+        def run_steps(k):
+            while k > 0:
+                c = min(C, k)
+                env.rollout(c, args.policy, 0.0, rewards=rew[:c], dones=dn[:c])
+                k -= c
+        run_steps(max(W, 1))
+        per_launch_steps = C
+
+    # ---------------- timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(K)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---------------- kernel duration for the roofline (events on the launch stream)
+    n_ev = 30
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    c1 = per_launch_steps
+    rew1 = torch.zeros((c1, B, NA), device=dev)
+    dn1 = torch.zeros((c1, B), dtype=torch.uint8, device=dev)
+    for a, b in evs:
+        a.record(stream)
+        env.rollout(c1, args.policy, 0.0, rewards=rew1, dones=dn1)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kms = sorted(a.elapsed_time(b) for a, b in evs)
+    kernel_ms = sum(kms[: n_ev // 2 + 1]) / (n_ev // 2 + 1)   # lower-median mean: drops launch jitter
+    if args.mode == "graph":
+        bytes_per_env_step = 2 * 4 * words + 4 * NA + 1
+        bytes_per_launch = B * bytes_per_env_step
+    else:
+        bytes_per_env_step = (2 * 4 * words + c1 * (4 * NA + 1)) / c1
+        bytes_per_launch = B * (2 * 4 * words + c1 * (4 * NA + 1))
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+
+    total_agent_steps = world * B * NA * K
+    value = total_agent_steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/u32 packed integer state, f32 rewards",
+            "data": "synthetic: philox-seeded episodes keyed by global env id, greedy policy on device",
+            "config": {
+                "workload": f"C3: {args.variant} N={NA}, B={B} envs/GPU, {args.policy} policy fused with "
+                            f"step + auto-reset (device-resident rollout)",
+                "envs_per_gpu": B, "agents": NA, "variant": args.variant, "policy": args.policy,
+                "launch": "hipGraph of 1-step launches" if args.mode == "graph" else f"{c1} steps per launch",
+                "parallelism": f"independent env shards x{world}, no collectives",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(f"{args.variant}_n{NA}_{args.mode}"),
+                "kernel": "k_step<Cfg<16,9,3,8>, greedy>" if args.variant == "medium" and NA == 8 else "k_step",
+                "kernel_ms": kernel_ms,
+                "bytes_per_launch": bytes_per_launch,
+                "bytes_per_env_step": bytes_per_env_step,
+            },
+        }
+        if not args.no_cpu_baseline:
+            procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(args.variant, NA, procs, args.cpu_seconds)
+            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

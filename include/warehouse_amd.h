@@ -1,0 +1,147 @@
+/*
+ * warehouse_amd.h -- C ABI of the MI355X (gfx950) batched warehouse simulator.
+ *
+ * Drop-in boundary for the hot path of ffahleraz/rllib-warehouse: `Warehouse.reset()` /
+ * `Warehouse.step()` (warehouse/core.py:167-442) and the greedy baseline policy
+ * (baseline/solvers.py:27-58), run for B independent episodes on one GPU.  Plain pointers and
+ * sizes only; every pointer named "device" is HIP device memory, `stream` is a hipStream_t
+ * (NULL = the default stream).  All calls are asynchronous on `stream` except where noted, return
+ * WH_OK (0) or a WH_E* code, and never throw.  The reference is Python, so the binding a maintainer
+ * adds on the reference side is ctypes; `warehouse/_native.py` is that binding.
+ *
+ * PACKED STATE (device, struct-of-arrays across the batch, word-plane major):
+ *   state[w * B + e] is 32-bit word w of env e, 0 <= w < wh_layout.words_per_env:
+ *     w = 0            header : bits 0-15 t (episode time, core.py:165), bits 16-23 n (live agents),
+ *                               bit 24 fresh (set by reset: observation availabilities read 0,
+ *                               core.py:233)
+ *     w = 1            episode counter (bumped by every reset; keys the philox streams)
+ *     w = 2 .. 2+NA-1  agent slot i: byte0 x, byte1 y, byte2 (delivery target + 1, 0 = idle)
+ *                      (core.py:153-154)
+ *     next P/4 words   pickup point j, byte j%4 of word j/4: (request target + 1, 0 = no request)
+ *                      (core.py:158)
+ *     next P/4 words   pickup point j: remaining wait (core.py:159; 0 when no request)
+ *   NA = cfg.agent_slots, P = 4 * num_racks^2.  Slots >= n are all-zero.
+ *
+ * RNG MODES.  Every draw the reference takes from numpy's global MT19937 stream can either be
+ * INJECTED (explicit arrays below: bit-exact parity with the reference given its draws) or taken
+ * from the PHILOX contract: Philox4x32-10 keyed by `seed`, counter (env_offset + e, episode, t,
+ * purpose << 24 | block); purposes RESET=1, REGEN=2, POLICY=3, RANDOM=4 (word layout in
+ * DESIGN.md §RNG and oracle/philox.py).  Philox trajectories depend only on the global env id,
+ * so any sharding of env ids over GPUs reproduces them exactly.
+ */
+#ifndef WAREHOUSE_AMD_H
+#define WAREHOUSE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WH_OK 0
+#define WH_EINVAL 22      /* bad pointer / size / value */
+#define WH_ENOTSUP 95     /* a layout this build has no kernel for */
+#define WH_EHIP 1000      /* + hipError_t: a HIP runtime error */
+
+#define WH_MAX_RACKS 8
+
+/* Variant geometry.  Mirrors the constructor of warehouse/core.py:78-86
+ * (the variant table is warehouse/variants.py:25-62). */
+typedef struct wh_config {
+  int32_t area_dimension;        /* D                          core.py:82 */
+  int32_t num_requests;          /* R (always-open requests)   core.py:81 */
+  int32_t num_racks;             /* len(pickup_racks_arrangement) */
+  int32_t racks[WH_MAX_RACKS];   /* pickup_racks_arrangement   core.py:83 */
+  int32_t agent_slots;           /* NA: agent records per env (num_agents, or max_num_agents for
+                                    the Train variants, variants.py:65-98); 1 <= NA <= R */
+  int32_t episode_duration;      /* T                          core.py:84 */
+  int32_t pickup_wait_duration;  /* W (<= 255)                 core.py:85 */
+} wh_config;
+
+typedef struct wh_layout {
+  int32_t words_per_env;   /* packed state words per env */
+  int32_t num_pickups;     /* P  = 4 * num_racks^2        core.py:96 */
+  int32_t num_deliveries;  /* Dp = 4 * (D - 4)            core.py:97 */
+  int32_t obs_len;         /* 9R + 1 floats per agent row, sorted gym.spaces.Dict key order */
+  int32_t kernel_agents;   /* compile-time agent bound of the kernel chosen for this config */
+} wh_layout;
+
+/* Validate `cfg` and describe its packed layout.  Host only, synchronous. */
+int wh_query(const wh_config* cfg, wh_layout* out);
+
+/* Canonical <-> packed state.  Canonical arrays are int32 device tensors:
+ *   pos [B,NA,2], agent_target [B,NA] (-1 idle), pickup_target [B,P] (-1 none),
+ *   pickup_timer [B,P] (-1 none), t [B], n [B]; fresh [B] uint8; episode [B] uint32.
+ * (the reference's own state arrays, core.py:150-165) */
+int wh_pack(const wh_config* cfg, int64_t B, const int32_t* pos, const int32_t* agent_target,
+            const int32_t* pickup_target, const int32_t* pickup_timer, const int32_t* t,
+            const int32_t* n, const uint8_t* fresh, const uint32_t* episode, uint32_t* state,
+            void* stream);
+int wh_unpack(const wh_config* cfg, int64_t B, const uint32_t* state, int32_t* pos,
+              int32_t* agent_target, int32_t* pickup_target, int32_t* pickup_timer, int32_t* t,
+              int32_t* n, uint8_t* fresh, uint32_t* episode, void* stream);
+
+/* Injected reset draws (core.py:191-221): accepted spawn cells, the R opened pickups and their
+ * targets in draw order, and (Train variants, variants.py:73-74) the agent count. */
+typedef struct wh_reset_draws {
+  const int32_t* spawn;    /* [B,NA,2] */
+  const int32_t* pickups;  /* [B,R]    distinct pickup indices */
+  const int32_t* targets;  /* [B,R]    delivery indices */
+  const int32_t* n;        /* [B] or NULL (= NA) */
+} wh_reset_draws;
+
+/* Warehouse.reset()  (warehouse/core.py:167-260; Train variants variants.py:69-71).
+ * mask [B] uint8 or NULL (all); draws NULL = philox; variable_n != 0 draws n ~ U{1..NA}. */
+int wh_reset(const wh_config* cfg, int64_t B, uint32_t* state, const uint8_t* mask,
+             const wh_reset_draws* draws, int32_t variable_n, uint64_t seed, int64_t env_offset,
+             void* stream);
+
+#define WH_PHASE_ALL 0        /* the whole of core.py:262-442 */
+#define WH_PHASE_PRE_REGEN 1  /* everything but regeneration (core.py:267-335, 354-442);
+                                 writes n_inactive so a host can draw the reference's
+                                 np.random.choice(inactive, k) before WH_PHASE_REGEN */
+#define WH_PHASE_REGEN 2      /* regeneration only (core.py:338-351) */
+
+/* Warehouse.step(action_dict)  (warehouse/core.py:262-442).
+ *   actions   [B,NA] int32 in 0..8 (MOVES index, core.py:38; the host wraps -9..-1 like Python)
+ *   order     [B,NA] int32 or NULL: action-dict iteration order (core.py:279), -1 terminated;
+ *             agents not listed do not move.  NULL = ascending agent id.
+ *   rewards   [B,NA] float32 (core.py:334-368), dones [B] uint8 (core.py:438); either may be NULL
+ *   regen     [B,2R] int32 or NULL (philox): R positions into the ascending list of inactive
+ *             pickups (the index np.random.choice(inactive,k) picked), then R delivery targets;
+ *             only the first k = R - P + |inactive| of each are read.
+ *   n_inactive [B] int32 or NULL: |inactive| before regeneration (core.py:338). */
+int wh_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
+            const int32_t* order, float* rewards, uint8_t* dones, const int32_t* regen,
+            int32_t* n_inactive, int32_t phase, uint64_t seed, int64_t env_offset, void* stream);
+
+/* Per-agent observation rows (core.py:224-260 after reset, 371-432 after a step, including the
+ * row-1 quirk of core.py:428), flattened in sorted-key order:
+ *   num_agents, other_availabilities, other_delivery_targets, other_positions, requests,
+ *   self_availability, self_delivery_target, self_position
+ * obs [B,NA,9R+1] float32; rows of slots >= n are zero. */
+int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* stream);
+
+#define WH_POLICY_GREEDY 1    /* baseline/solvers.py:27-58 with random_action_prob p */
+#define WH_POLICY_RANDOM 2    /* uniform over the 9 moves (action_space.sample()) */
+
+/* WarehouseRandomGreedySolver.compute_action (baseline/solvers.py:27-58) evaluated on the state,
+ * or uniform random actions: writes actions [B,NA] int32 (slots >= n get 4 = stay). */
+int wh_policy(const wh_config* cfg, int64_t B, const uint32_t* state, int32_t policy, float p,
+              int32_t* actions, uint64_t seed, int64_t env_offset, void* stream);
+
+/* Device-resident rollout: `steps` iterations of {policy, step, auto-reset at t >= T} in one
+ * launch (the loop of baseline/run.py:42-62 without the host).  State stays in registers between
+ * iterations.  rewards [steps,B,NA] / dones [steps,B] / returns [B] (+= sum of rewards) may each
+ * be NULL.  Philox draws only. */
+int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy,
+               float p, float* rewards, uint8_t* dones, float* returns, int32_t autoreset,
+               int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
+
+/* Library build identification (e.g. "warehouse_amd gfx950 <date>"). */
+const char* wh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAREHOUSE_AMD_H */

@@ -86,15 +86,15 @@ def _bits(idx):
     return np.left_shift(U64(1), np.asarray(idx, np.int64).astype(U64))
 
 
-def _choose_without_replacement(avail_mask, count, words_fn, k_needed, first_word):
-    """Sequential r-th-remaining selection used by the philox contract."""
+def _choose_without_replacement(avail_mask, count, words_fn, k_needed, first_word, stride=2):
+    """Sequential r-th-remaining selection used by the philox contract (word first + stride*j)."""
     B = avail_mask.shape[0]
     R = k_needed.max(initial=0)
     sel = np.full((B, max(R, 0)), -1, np.int64)
     rem = avail_mask.copy()
     for j in range(R):
         act = j < k_needed
-        w = words_fn(first_word + j)
+        w = words_fn(first_word + stride * j)
         r = ph.uniform_int(np.maximum(count - j, 1), w)
         s = ph.select_bit(rem, r)
         s = np.where(act, s, -1)
@@ -124,7 +124,7 @@ def reset(L: Layout, S: BState, draws, mask: Optional[np.ndarray] = None, nmax: 
         full_d = np.full(B, U64((1 << L.Dp) - 1 if L.Dp < 64 else 0xFFFFFFFFFFFFFFFF), U64)
         kR = np.full(B, L.R)
         sel = _choose_without_replacement(full_p, L.P, wf, kR, 1 + NA)
-        tgt = _choose_without_replacement(full_d, L.Dp, wf, kR, 1 + NA + L.R)
+        tgt = _choose_without_replacement(full_d, L.Dp, wf, kR, 2 + NA)
     else:
         n = np.asarray(draws.n if draws.n is not None else np.full(B, n_fixed or NA), np.int64)
         spawn = np.asarray(draws.spawn, np.int32)
@@ -145,8 +145,7 @@ def reset(L: Layout, S: BState, draws, mask: Optional[np.ndarray] = None, nmax: 
     S.t[m] = 0
     S.n[m] = n[m]
     S.fresh[m] = True
-    if isinstance(draws, PhiloxDraws):
-        S.episode[m] = ep[m].astype(np.uint32)
+    S.episode[m] = ep[m].astype(np.uint32)   # every reset bumps the episode counter
 
 
 # --------------------------------------------------------------------------- step
@@ -225,7 +224,7 @@ def step(L: Layout, S: BState, actions: np.ndarray, draws, order: Optional[np.nd
         wf = lambda j: draws.word(S.episode, t_new, ph.REGEN, j)  # noqa: E731
         sel = _choose_without_replacement(imask, n_in, wf, k, 0)
         full_d = np.full(B, U64((1 << L.Dp) - 1 if L.Dp < 64 else 0xFFFFFFFFFFFFFFFF), U64)
-        tg = _choose_without_replacement(full_d, L.Dp, wf, k, R)
+        tg = _choose_without_replacement(full_d, L.Dp, wf, k, 1)
     else:
         rpos = np.asarray(draws.rpos, np.int64)
         tg = np.asarray(draws.rtgt, np.int64)

@@ -15,10 +15,11 @@ include/warehouse_amd.h and DESIGN.md.
 Streams (purpose, t):
   RESET   (1, 0)      word 0: n = 1 + uniform_int(nmax, .) (Train variants only)
                       word 1+i: spawn cell of agent slot i = valid_cells[uniform_int(n_valid, .)]
-                      word 1+NA+j: j-th request pickup = r-th not-yet-chosen pickup, r = uniform_int(P-j)
-                      word 1+NA+R+j: its target = r-th not-yet-chosen delivery point, r = uniform_int(Dp-j)
-  REGEN   (2, t_new)  word j (<k): j-th reopened pickup = r-th remaining inactive, r = uniform_int(n_in-j)
-                      word R+j: its target = r-th target not chosen in this regeneration, r = uniform_int(Dp-j)
+                      word 1+NA+2j: j-th request pickup = r-th not-yet-chosen pickup, r = uniform_int(P-j)
+                      word 2+NA+2j: its target = r-th not-yet-chosen delivery point, r = uniform_int(Dp-j)
+  REGEN   (2, t_new)  word 2j (j<k): j-th reopened pickup = r-th remaining inactive, r = uniform_int(n_in-j)
+                      word 2j+1: its target = r-th target not chosen in this regeneration, r = uniform_int(Dp-j)
+  (pickup and target words interleave so the usual k <= 2 reopenings cost one Philox block)
   POLICY  (3, t_obs)  word 2i: coin u = (w >> 8) / 2**24, random iff u < p; word 2i+1: action uniform_int(9)
   RANDOM  (4, t_obs)  word i: action uniform_int(9)
 """

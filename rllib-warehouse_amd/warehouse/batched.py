@@ -1,0 +1,176 @@
+"""B independent warehouse episodes resident on one MI355X.
+
+`BatchedWarehouse` owns the packed struct-of-arrays state (include/warehouse_amd.h, "PACKED
+STATE") as one int32 device tensor `state[words, B]` and drives the HIP kernels through the C ABI:
+
+    reset()    -> wh_reset    Warehouse.reset()              warehouse/core.py:167-260
+    step()     -> wh_step     Warehouse.step()               warehouse/core.py:262-442
+    observe()  -> wh_observe  per-agent observation rows     warehouse/core.py:224-260, 371-432
+    policy()   -> wh_policy   greedy / random actions        baseline/solvers.py:27-58
+    rollout()  -> wh_rollout  device-resident rollout loop   baseline/run.py:42-62
+
+Global env ids are `env_offset + e`; with philox draws a shard of env ids reproduces exactly the
+trajectories those ids have in any other sharding (multi-GPU is a straight per-device shard).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from ._geometry import GEOMETRY
+
+POLICIES = {"greedy": nat.WH_POLICY_GREEDY, "random": nat.WH_POLICY_RANDOM}
+
+
+def require_device(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("warehouse: no HIP device visible -- the simulator runs only on an "
+                           "MI355X (gfx950); there is no CPU fallback")
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise RuntimeError(f"warehouse: device {dev} is not a HIP device")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def _dev_i32(x, device, shape=None):
+    if x is None:
+        return None
+    t = torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x)
+    t = t.to(device=device, dtype=torch.int32).contiguous()
+    if shape is not None:
+        t = t.reshape(shape)
+    return t
+
+
+class BatchedWarehouse:
+    """`num_envs` episodes of one variant.  `train=True` gives the Train variants' per-episode
+    agent count n ~ U{1..max_num_agents} (warehouse/variants.py:65-98) with max_num_agents slots."""
+
+    def __init__(self, variant: str = "medium", num_envs: int = 1, num_agents: Optional[int] = None,
+                 *, train: bool = False, seed: int = 0, env_offset: int = 0, device=None,
+                 geometry: Optional[dict] = None):
+        geo = dict(GEOMETRY[variant] if geometry is None else geometry)
+        self.geometry = geo
+        self.train = bool(train)
+        nmax = int(geo["max_agents"])
+        slots = nmax if train or num_agents is None else int(num_agents)
+        if not 1 <= slots <= geo["R"]:
+            raise AssertionError("num_agents <= num_requests (core.py:89)")
+        self.agent_slots = slots
+        self.cfg = nat.make_config(geo["D"], geo["R"], geo["racks"], slots, geo["T"], geo["W"])
+        self.layout = nat.query(self.cfg)
+        self.device = require_device(device)
+        self.B = int(num_envs)
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self.R, self.P, self.Dp = geo["R"], self.layout.num_pickups, self.layout.num_deliveries
+        self.obs_len = self.layout.obs_len
+        self.state = torch.zeros((self.layout.words_per_env, self.B), dtype=torch.int32, device=self.device)
+        self.rewards = torch.zeros((self.B, slots), dtype=torch.float32, device=self.device)
+        self.dones = torch.zeros(self.B, dtype=torch.uint8, device=self.device)
+        self.actions = torch.full((self.B, slots), 4, dtype=torch.int32, device=self.device)
+        self.n_inactive = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self._obs = None
+        self._cfgp = ctypes.byref(self.cfg)
+
+    # ------------------------------------------------------------------ plumbing
+    @property
+    def stream(self) -> int:
+        return nat.stream_of(self.device)
+
+    def _call(self, name, *args):
+        nat.check(getattr(nat.lib(), name)(self._cfgp, self.B, *args), name)
+
+    # ------------------------------------------------------------------ API
+    def reset(self, mask=None, draws: Optional[Dict[str, object]] = None) -> None:
+        """Reset the envs selected by `mask` ([B] bool; None = all).  `draws` injects the
+        reference's reset draws: spawn [B,NA,2], pickups [B,R], targets [B,R], n [B] (optional)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        keep = []
+        dp = None
+        if draws is not None:
+            sp = _dev_i32(draws["spawn"], self.device, (self.B, self.agent_slots, 2))
+            pk = _dev_i32(draws["pickups"], self.device, (self.B, self.R))
+            tg = _dev_i32(draws["targets"], self.device, (self.B, self.R))
+            nn = _dev_i32(draws.get("n"), self.device, (self.B,))
+            keep = [sp, pk, tg, nn]
+            dp = ctypes.byref(nat.WhResetDraws(sp.data_ptr(), pk.data_ptr(), tg.data_ptr(),
+                                               None if nn is None else nn.data_ptr()))
+        self._call("wh_reset", self.state.data_ptr(), nat.ptr(m), dp, int(self.train),
+                   self.seed, self.env_offset, self.stream)
+        del keep
+
+    def step(self, actions, order=None, regen=None, phase: int = nat.WH_PHASE_ALL
+             ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One transition for every env.  actions [B,NA] in 0..8; order [B,NA] (-1 padded) is the
+        action-dict iteration order; regen [B,2R] injects the regeneration draws.  Returns the
+        env-owned (rewards [B,NA] float32, dones [B] uint8) buffers, overwritten next call."""
+        a = None if actions is None else _dev_i32(actions, self.device, (self.B, self.agent_slots))
+        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
+        r = _dev_i32(regen, self.device, (self.B, 2 * self.R))
+        self._call("wh_step", self.state.data_ptr(), nat.ptr(a), nat.ptr(o), self.rewards.data_ptr(),
+                   self.dones.data_ptr(), nat.ptr(r), self.n_inactive.data_ptr(), int(phase),
+                   self.seed, self.env_offset, self.stream)
+        return self.rewards, self.dones
+
+    def observe(self) -> torch.Tensor:
+        """[B, NA, 9R+1] float32 rows in sorted-key order (env-owned buffer)."""
+        if self._obs is None:
+            self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
+                                    device=self.device)
+        self._call("wh_observe", self.state.data_ptr(), self._obs.data_ptr(), self.stream)
+        return self._obs
+
+    def policy(self, kind: str = "greedy", p: float = 0.0) -> torch.Tensor:
+        self._call("wh_policy", self.state.data_ptr(), POLICIES[kind], float(p), self.actions.data_ptr(),
+                   self.seed, self.env_offset, self.stream)
+        return self.actions
+
+    def rollout(self, steps: int, policy: str = "greedy", p: float = 0.0, rewards=None, dones=None,
+                returns=None, autoreset: bool = True) -> None:
+        """`steps` fused iterations of {policy, step, auto-reset}.  rewards [steps,B,NA] float32,
+        dones [steps,B] uint8 and returns [B] float32 (+=) are optional device tensors."""
+        for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
+                         (returns, (self.B,))):
+            if t is not None and tuple(t.shape) != shape:
+                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+        self._call("wh_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
+                   nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns), int(bool(autoreset)),
+                   int(self.train), self.seed, self.env_offset, self.stream)
+
+    # ------------------------------------------------------------------ canonical state
+    def to_canonical(self) -> Dict[str, torch.Tensor]:
+        B, NA, P = self.B, self.agent_slots, self.P
+        z = dict(pos=torch.empty((B, NA, 2), dtype=torch.int32, device=self.device),
+                 agent_target=torch.empty((B, NA), dtype=torch.int32, device=self.device),
+                 pickup_target=torch.empty((B, P), dtype=torch.int32, device=self.device),
+                 pickup_timer=torch.empty((B, P), dtype=torch.int32, device=self.device),
+                 t=torch.empty(B, dtype=torch.int32, device=self.device),
+                 n=torch.empty(B, dtype=torch.int32, device=self.device),
+                 fresh=torch.empty(B, dtype=torch.uint8, device=self.device),
+                 episode=torch.empty(B, dtype=torch.int32, device=self.device))
+        self._call("wh_unpack", self.state.data_ptr(), *(z[k].data_ptr() for k in
+                   ("pos", "agent_target", "pickup_target", "pickup_timer", "t", "n", "fresh", "episode")),
+                   self.stream)
+        return z
+
+    def from_canonical(self, c: Dict[str, object]) -> None:
+        B, NA, P = self.B, self.agent_slots, self.P
+        d = self.device
+        t = dict(pos=_dev_i32(c["pos"], d, (B, NA, 2)), agent_target=_dev_i32(c["agent_target"], d, (B, NA)),
+                 pickup_target=_dev_i32(c["pickup_target"], d, (B, P)),
+                 pickup_timer=_dev_i32(c["pickup_timer"], d, (B, P)), t=_dev_i32(c["t"], d, (B,)),
+                 n=_dev_i32(c.get("n", np.full(B, NA)), d, (B,)),
+                 fresh=torch.as_tensor(np.asarray(c.get("fresh", np.zeros(B, bool)))).to(d, torch.uint8).contiguous(),
+                 episode=_dev_i32(c.get("episode", np.zeros(B, np.int64)), d, (B,)))
+        self._call("wh_pack", *(t[k].data_ptr() for k in
+                   ("pos", "agent_target", "pickup_target", "pickup_timer", "t", "n", "fresh", "episode")),
+                   self.state.data_ptr(), self.stream)

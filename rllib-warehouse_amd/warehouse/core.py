@@ -1,0 +1,157 @@
+"""Drop-in `Warehouse` (RLlib MultiAgentEnv) backed by the gfx950 kernels.
+
+Same constructor, attributes and reset()/step() contract as the reference class
+(warehouse/core.py:73-442), so baseline/run.py and scripts/train.py run unchanged.  One env is a
+B=1 batch of `BatchedWarehouse`; every transition runs on the GPU.
+
+RNG parity.  The reference draws from numpy's GLOBAL stream (core.py:196-197, 215-220, 339-350),
+interleaved with whatever else the process draws (e.g. the greedy solver's per-agent coin,
+solvers.py:44).  To keep seeded trajectories identical, this class takes exactly those draws from
+np.random on the host, in the same order, and injects them into the kernels:
+  reset(): spawn rejection loop + choice(P, R) + choice(Dp, R)        -> wh_reset (injected)
+  step():  wh_step(WH_PHASE_PRE_REGEN) reports |inactive|, then
+           choice(|inactive|, k) + choice(Dp, k) on the host          -> wh_step(WH_PHASE_REGEN)
+For thousands of envs use `warehouse.batched.BatchedWarehouse` (device philox draws) instead.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from ._compat import MultiAgentEnv, spaces
+from ._geometry import pickup_cells
+from .batched import BatchedWarehouse
+
+__all__ = ["Warehouse"]
+
+ANIMATE_FRAMES_PER_STEP: int = 10     # core.py:69-70
+ANIMATE_STEPS_PER_SECOND: float = 6.0
+
+OBS_KEYS = ("num_agents", "other_availabilities", "other_delivery_targets", "other_positions",
+            "requests", "self_availability", "self_delivery_target", "self_position")
+
+
+def _default_device():
+    return os.environ.get("WAREHOUSE_DEVICE", "cuda")
+
+
+class Warehouse(MultiAgentEnv):
+    metadata = {"render.modes": ["human"]}
+
+    def __init__(self, num_agents: int, num_requests: int, area_dimension: int,
+                 pickup_racks_arrangement: List[int], episode_duration: int,
+                 pickup_wait_duration: int) -> None:
+        super(Warehouse, self).__init__()
+        assert num_agents <= num_requests
+
+        self._area_dimension = int(area_dimension)
+        self._pickup_racks_arrangement = list(pickup_racks_arrangement)
+        self._num_agents = int(num_agents)
+        self._num_requests = int(num_requests)
+        self._num_pickup_points = 4 * len(self._pickup_racks_arrangement) ** 2
+        self._num_delivery_points = 4 * int(self._area_dimension - 4)
+        self._episode_duration = int(episode_duration)
+        self._pickup_wait_duration = int(pickup_wait_duration)
+        self._null_position = self._area_dimension // 2
+
+        self.num_agents = self._num_agents
+        self.num_requests = self._num_requests
+        self.animate_frames_per_step = ANIMATE_FRAMES_PER_STEP
+        self.animate_steps_per_second = ANIMATE_STEPS_PER_SECOND
+
+        R, D = self._num_requests, self._area_dimension
+        self.reward_range = (0.0, 1.0)
+        self.action_space = spaces.Discrete(9)
+        self.observation_space = spaces.Dict({
+            "num_agents": spaces.Box(low=1, high=R, shape=(1,), dtype=np.int32),
+            "self_position": spaces.Box(low=0, high=D, shape=(2,), dtype=np.int32),
+            "self_availability": spaces.MultiBinary(1),
+            "self_delivery_target": spaces.Box(low=0, high=D, shape=(2,), dtype=np.int32),
+            "other_positions": spaces.Box(low=0, high=D, shape=(R - 1, 2), dtype=np.int32),
+            "other_availabilities": spaces.MultiBinary(R - 1),
+            "other_delivery_targets": spaces.Box(low=0, high=D, shape=(R - 1, 2), dtype=np.int32),
+            "requests": spaces.Box(low=0, high=D, shape=(R, 4), dtype=np.int32),
+        })
+
+        self._pickup_set = set(pickup_cells(D, self._pickup_racks_arrangement))
+        geo = dict(D=D, R=R, racks=tuple(self._pickup_racks_arrangement), T=self._episode_duration,
+                   W=self._pickup_wait_duration, max_agents=self._num_agents)
+        self._engine = BatchedWarehouse(num_envs=1, num_agents=self._num_agents, geometry=geo,
+                                        device=_default_device())
+        w = {k: n for k, n in zip(OBS_KEYS, (1, R - 1, 2 * (R - 1), 2 * (R - 1), 4 * R, 1, 2, 2))}
+        self._obs_split = np.cumsum([w[k] for k in OBS_KEYS])[:-1]
+        self._done = False
+
+    # ------------------------------------------------------------------ helpers
+    def _obs_dicts(self) -> Dict[str, Dict[str, np.ndarray]]:
+        rows = self._engine.observe()[0].cpu().numpy().astype(np.int32)
+        R = self._num_requests
+        out = {}
+        for i in range(self._num_agents):
+            p = np.split(rows[i], self._obs_split)
+            out[str(i)] = {
+                "num_agents": p[0],
+                "self_position": p[7],
+                "self_availability": p[5].astype(np.int8),
+                "self_delivery_target": p[6],
+                "other_positions": p[3].reshape(R - 1, 2),
+                "other_availabilities": p[1].astype(np.int8),
+                "other_delivery_targets": p[2].reshape(R - 1, 2),
+                "requests": p[4].reshape(R, 4),
+            }
+        return out
+
+    # ------------------------------------------------------------------ MultiAgentEnv
+    def reset(self) -> Dict[str, Dict[str, np.ndarray]]:
+        D, R, n = self._area_dimension, self._num_requests, self._num_agents
+        spawn = []
+        for _ in range(n):                                  # core.py:191-201, same draw order
+            while True:
+                cell = (np.random.randint(1, D - 1), np.random.randint(1, D - 1))
+                if cell not in self._pickup_set:
+                    spawn.append(cell)
+                    break
+        sel = np.random.choice(self._num_pickup_points, R, replace=False)      # core.py:215-217
+        tgt = np.random.choice(self._num_delivery_points, R, replace=False)    # core.py:218-220
+        self._engine.reset(draws=dict(spawn=np.array(spawn, np.int32).reshape(1, n, 2),
+                                      pickups=sel.reshape(1, R), targets=tgt.reshape(1, R)))
+        return self._obs_dicts()
+
+    def step(self, action_dict: Dict[str, int]
+             ) -> Tuple[Dict[str, dict], Dict[str, float], Dict[str, bool], Dict[str, dict]]:
+        n, R = self._num_agents, self._num_requests
+        order = np.full((1, n), -1, np.int32)
+        acts = np.full((1, n), 4, np.int32)
+        for s, (key, action) in enumerate(action_dict.items()):
+            idx = int(key)
+            a = int(action)
+            if not -9 <= a <= 8:                            # MOVES[action] (core.py:282)
+                raise IndexError("list index out of range")
+            if not 0 <= idx < n:
+                raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
+            order[0, s] = idx
+            acts[0, idx] = a % 9                             # Python's negative-index wrap
+        eng = self._engine
+        eng.step(acts, order=order, phase=nat.WH_PHASE_PRE_REGEN)
+        n_in = int(eng.n_inactive[0].item())
+        k = R - self._num_pickup_points + n_in
+        rpos = np.random.choice(n_in, k, replace=False)                       # core.py:339-343
+        rtgt = np.random.choice(self._num_delivery_points, k, replace=False)  # core.py:346-350
+        regen = np.full((1, 2 * R), -1, np.int32)
+        regen[0, :k] = rpos
+        regen[0, R:R + k] = rtgt
+        eng.step(None, regen=regen, phase=nat.WH_PHASE_REGEN)
+        obs = self._obs_dicts()
+        rew = eng.rewards[0].cpu().numpy()
+        done = bool(eng.dones[0].item())
+        rewards = {str(i): rew[i] for i in range(n)}
+        dones = {str(i): done for i in range(n)}
+        dones["__all__"] = done
+        return obs, rewards, dones, {str(i): {} for i in range(n)}
+
+    def render(self, mode: str = "human", animate: bool = False) -> None:
+        raise NotImplementedError("rendering (core.py:444-617) is out of scope for the GPU build")

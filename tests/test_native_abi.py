@@ -1,0 +1,80 @@
+"""CPU-side checks of the C ABI: the library loads, exports exactly what include/warehouse_amd.h
+declares, and validates configurations host-side (no device calls)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "warehouse_amd.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(wh_[a-z_]+)\s*\(", text, flags=re.M)))
+
+
+def test_header_symbols_match_binding():
+    from warehouse import _native
+
+    assert declared_symbols() == sorted(_native.SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    from warehouse import _native
+
+    lib = _native.lib()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (wh_[a-z_]+)$", out, flags=re.M))
+    assert exported == set(declared_symbols())
+    assert _native.lib().wh_version().startswith(b"warehouse_amd gfx950")
+
+
+@pytest.mark.parametrize("variant", ["small", "medium", "large"])
+def test_query_layouts(variant):
+    from warehouse import _native
+    from warehouse._geometry import GEOMETRY
+
+    g = GEOMETRY[variant]
+    for na in range(1, g["max_agents"] + 1):
+        cfg = _native.make_config(g["D"], g["R"], g["racks"], na, g["T"], g["W"])
+        lo = _native.query(cfg)
+        P = 4 * len(g["racks"]) ** 2
+        assert lo.num_pickups == P and lo.num_deliveries == 4 * (g["D"] - 4)
+        assert lo.words_per_env == 2 + na + 2 * (P // 4)
+        assert lo.obs_len == 9 * g["R"] + 1
+        assert lo.kernel_agents >= na
+
+
+def test_query_rejects_bad_configs():
+    from warehouse import _native
+
+    bad = [
+        (12, 4, (4, 8), 5, 200, 200),      # more agents than requests (core.py:89)
+        (12, 4, (4, 8), 0, 200, 200),      # no agents
+        (12, 4, (4, 8), 2, 200, 0),        # zero wait
+        (12, 4, (4, 8), 2, 200, 256),      # W does not fit the 8-bit timer plane
+    ]
+    for c in bad:
+        with pytest.raises(ValueError):
+            _native.query(_native.make_config(*c))
+    with pytest.raises(_native.WarehouseNativeError):   # racks on the border: no kernel for it
+        _native.query(_native.make_config(12, 4, (1, 8), 2, 200, 200))
+    with pytest.raises(_native.WarehouseNativeError):   # geometry with no compiled kernel
+        _native.query(_native.make_config(14, 4, (4, 8), 2, 200, 200))
+
+
+def test_no_cpu_fallback():
+    import torch
+    import warehouse
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        warehouse.BatchedWarehouse("small", 4, 2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        warehouse.WarehouseSmall(2)
