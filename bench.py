@@ -172,19 +172,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---------------- kernel duration for the roofline (events on the launch stream)
-    n_ev = 30
+    # ---------------- kernel duration for the roofline: HIP events on the launch stream around
+    # back-to-back launches (graph replays of G one-step launches, or single fused launches)
+    n_ev = 7
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     c1 = per_launch_steps
-    rew1 = torch.zeros((c1, B, NA), device=dev)
-    dn1 = torch.zeros((c1, B), dtype=torch.uint8, device=dev)
-    for a, b in evs:
-        a.record(stream)
-        env.rollout(c1, args.policy, 0.0, rewards=rew1, dones=dn1)
-        b.record(stream)
+    if args.mode == "graph":
+        launches_per_ev = G
+        for a, b in evs:
+            a.record(stream)
+            graph.replay()
+            b.record(stream)
+    else:
+        launches_per_ev = 1
+        for a, b in evs:
+            a.record(stream)
+            env.rollout(c1, args.policy, 0.0, rewards=rew, dones=dn)
+            b.record(stream)
     torch.cuda.synchronize(dev)
-    kms = sorted(a.elapsed_time(b) for a, b in evs)
-    kernel_ms = sum(kms[: n_ev // 2 + 1]) / (n_ev // 2 + 1)   # lower-median mean: drops launch jitter
+    kms = sorted(a.elapsed_time(b) / launches_per_ev for a, b in evs)
+    kernel_ms = kms[n_ev // 2]   # median
     if args.mode == "graph":
         bytes_per_env_step = 2 * 4 * words + 4 * NA + 1
         bytes_per_launch = B * bytes_per_env_step

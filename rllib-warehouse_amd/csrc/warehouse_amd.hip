@@ -250,13 +250,14 @@ template <class C>
 __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e, int na, const int32_t* spawn,
                                const int32_t* pickups, const int32_t* targets, const int32_t* nn,
                                uint32_t W, int tid) {
-  const uint32_t n = nn ? (uint32_t)nn[e] : (uint32_t)na;
+  const uint32_t n = nn ? min((uint32_t)nn[e], (uint32_t)na) : (uint32_t)na;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) {
     uint32_t a = 0;
     if (i < na && i < (int)n) {
-      const uint32_t x = (uint32_t)spawn[(e * na + i) * 2], y = (uint32_t)spawn[(e * na + i) * 2 + 1];
-      a = (x & 0xFFu) | ((y & 0xFFu) << 8);
+      const uint32_t x = min((uint32_t)spawn[(e * na + i) * 2], (uint32_t)(C::D - 1));
+      const uint32_t y = min((uint32_t)spawn[(e * na + i) * 2 + 1], (uint32_t)(C::D - 1));
+      a = x | (y << 8);
     }
     s.ag[i] = a;
   }
@@ -266,6 +267,7 @@ __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e,
   for (int j = 0; j < C::R; ++j) {
     const uint32_t sel = (uint32_t)pickups[e * C::R + j];
     const uint32_t tg = (uint32_t)targets[e * C::R + j];
+    if (sel >= (uint32_t)C::P || tg >= (uint32_t)C::DP) continue;   // invalid injected draw: ignored
     opened |= 1ull << sel;
     *L.ptl_byte(sel, tid) = (uint8_t)(tg + 1);
   }
@@ -399,7 +401,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       int who = sidx;
       if (ordered) {
         who = (sidx < na) ? order[e * na + sidx] : -1;
-        live = who >= 0 && who < (int)n;
+        live = who >= 0 && who < (int)n && who < C::NAM;
         who = live ? who : 0;
         a = L.agl[who][tid];
         mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
@@ -495,8 +497,10 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         if (j < kreq) {
           int sel, tg;
           if (regen) {
-            sel = select_bit64(inactive, (uint32_t)regen[e * 2 * C::R + j]);
+            const uint32_t rp = (uint32_t)regen[e * 2 * C::R + j];
+            sel = rp < nin ? select_bit64(inactive, rp) : C::P;       // out-of-range draw: ignored
             tg = regen[e * 2 * C::R + C::R + j];
+            if ((uint32_t)tg >= (uint32_t)C::DP) sel = C::P;
           } else {
             if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, tnew, PUR_REGEN, (uint32_t)(j >> 1));
             const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
@@ -505,8 +509,10 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             tg = select_bit64(~used & low_mask<C::DP>(), __umulhi(w2, (uint32_t)(C::DP - j)));
             used |= 1ull << tg;
           }
-          opened |= 1ull << sel;
-          *L.ptl_byte((uint32_t)sel, tid) = (uint8_t)(tg + 1);
+          if (sel < C::P) {
+            opened |= 1ull << sel;
+            *L.ptl_byte((uint32_t)sel, tid) = (uint8_t)(tg + 1);
+          }
         }
       }
       if (opened) {
@@ -587,8 +593,9 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t act[C::NAM];
     if (POLICY == POL_EXTERNAL) {
+      const bool have = a.phase != PH_REGEN && a.order == nullptr;   // REGEN reads no actions
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) act[i] = (i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
+      for (int i = 0; i < C::NAM; ++i) act[i] = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
     } else {
       policy_actions<C, POLICY>(s, L, k, gid, a.p, act);
     }
@@ -751,7 +758,7 @@ struct PackParams {
   uint32_t* state;
   const uint32_t* cstate;
   int64_t B;
-  int32_t na, P, pw;
+  int32_t na, P, pw, D;
   int32_t *pos, *agent_target, *pickup_target, *pickup_timer, *t, *n;
   uint8_t* fresh;
   uint32_t* episode;
@@ -761,15 +768,17 @@ __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
   const int64_t e = (int64_t)blockIdx.x * BT + threadIdx.x;
   if (e >= a.B) return;
   const int64_t B = a.B;
-  const uint32_t n = (uint32_t)a.n[e];
-  a.state[e] = ((uint32_t)a.t[e] & 0xFFFFu) | ((n & 0xFFu) << 16) | (a.fresh[e] ? (1u << 24) : 0u);
+  // out-of-range canonical values are clamped so packed state always indexes inside the grid
+  const uint32_t n = min((uint32_t)max(a.n[e], 0), (uint32_t)a.na);
+  a.state[e] = ((uint32_t)a.t[e] & 0xFFFFu) | (n << 16) | (a.fresh[e] ? (1u << 24) : 0u);
   a.state[B + e] = a.episode[e];
   for (int i = 0; i < a.na; ++i) {
     uint32_t w = 0;
     if (i < (int)n) {
       const int32_t tg = a.agent_target[e * a.na + i];
-      w = ((uint32_t)a.pos[(e * a.na + i) * 2] & 0xFFu) | (((uint32_t)a.pos[(e * a.na + i) * 2 + 1] & 0xFFu) << 8) |
-          ((uint32_t)(tg + 1) << 16);
+      const uint32_t x = (uint32_t)min(max(a.pos[(e * a.na + i) * 2], 0), a.D - 1);
+      const uint32_t y = (uint32_t)min(max(a.pos[(e * a.na + i) * 2 + 1], 0), a.D - 1);
+      w = x | (y << 8) | ((uint32_t)min(max(tg + 1, 0), 255) << 16);
     }
     a.state[(2 + i) * B + e] = w;
   }
@@ -779,7 +788,7 @@ __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
       const int j = 4 * w + b;
       const int32_t tg = a.pickup_target[e * a.P + j];
       if (tg >= 0) {
-        tw |= (uint32_t)(tg + 1) << (8 * b);
+        tw |= (uint32_t)min(tg + 1, 255) << (8 * b);
         mw |= ((uint32_t)a.pickup_timer[e * a.P + j] & 0xFFu) << (8 * b);
       }
     }
@@ -997,7 +1006,7 @@ int wh_pack(const wh_config* cfg, int64_t B, const int32_t* pos, const int32_t* 
   if (B < 0 || !pos || !agent_target || !pickup_target || !pickup_timer || !t || !n || !fresh ||
       !episode || !state)
     return WH_EINVAL;
-  PackParams a{state, nullptr, B, g.NA, g.P, g.P / 4, const_cast<int32_t*>(pos),
+  PackParams a{state, nullptr, B, g.NA, g.P, g.P / 4, g.D, const_cast<int32_t*>(pos),
                const_cast<int32_t*>(agent_target), const_cast<int32_t*>(pickup_target),
                const_cast<int32_t*>(pickup_timer), const_cast<int32_t*>(t), const_cast<int32_t*>(n),
                const_cast<uint8_t*>(fresh), const_cast<uint32_t*>(episode)};
@@ -1015,7 +1024,7 @@ int wh_unpack(const wh_config* cfg, int64_t B, const uint32_t* state, int32_t* p
   if (B < 0 || !pos || !agent_target || !pickup_target || !pickup_timer || !t || !n || !fresh ||
       !episode || !state)
     return WH_EINVAL;
-  PackParams a{nullptr, state, B, g.NA, g.P, g.P / 4, pos, agent_target, pickup_target,
+  PackParams a{nullptr, state, B, g.NA, g.P, g.P / 4, g.D, pos, agent_target, pickup_target,
                pickup_timer, t, n, fresh, episode};
   hipLaunchKernelGGL(k_unpack, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());
