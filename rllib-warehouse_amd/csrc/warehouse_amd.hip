@@ -1,22 +1,29 @@
 // warehouse_amd.hip -- gfx950 kernels + C ABI for the batched warehouse hot path.
 //
-// Design (DESIGN.md has the full rationale and measurements):
+// Design (DESIGN.md has the rationale and the measurements behind each choice):
 //  * ONE LANE PER ENV.  The per-env work of core.py:262-442 is a short, mostly serial integer
-//    program (sequential collision resolution over agents, core.py:279-300).  Putting one env on
-//    one lane and the batch across lanes makes every HBM access a fully coalesced word-plane
-//    (state[w * B + e]) and shares each issued instruction among 64 envs.
+//    program (sequential collision resolution, core.py:279-300).  One env per lane with the batch
+//    across lanes makes every HBM access a coalesced word plane (state[w * B + e]) and shares each
+//    issued instruction among 64 envs.  With B = 65,536 that is one wave per SIMD, so the kernel
+//    is VALU-issue bound and every instruction per env-step counts.
+//  * 16-bit coordinate pairs.  An agent word is x | dx<<8 | y<<16 | dy<<24 (dx,dy = delivery
+//    target cell, 0xFF = idle): a move is 3 packed-i16 ops (the reference's "keep the old
+//    coordinate off the grid" rule equals a clamp for +-1 moves, core.py:282-287), a delivery test
+//    is one compare (core.py:354-362) and Manhattan distance is one v_sad_hi_u8, which also
+//    carries the pickup index and cell as a 16-bit tag so a v_min gives argmin-first-wins
+//    (solvers.py:53-58).
 //  * SWAR on packed bytes.  Pickup tables are 1 byte per point, 4 per register: expiry
-//    (core.py:303-306), pickup clearing and regeneration masks (core.py:330-351) run 4 points per
-//    VALU op; active/inactive sets are 64-bit masks (P <= 64).
-//  * v_sad_u8 for the greedy policy: |dx|+|dy| of byte-packed (x,y) in one instruction
-//    (solvers.py:53-58), argmin-first-wins as a v_min over (dist << 24 | index << 16 | xy).
-//  * Per-lane LDS scratch for the few data-dependent lookups (occupancy grid bits core.py:275-291,
-//    pickup target bytes core.py:327-329), laid out [word][lane] so every lane hits its own bank.
+//    (core.py:303-306) and clearing/opening (core.py:330-351) run 4 points per VALU op; the set of
+//    open requests is a 64-bit mask kept in registers across fused steps.
+//  * Per-lane LDS scratch for the data-dependent lookups (occupancy rows core.py:275-291, pickup
+//    target bytes core.py:327-329), laid out [word][lane] so every lane hits its own bank, and no
+//    data-dependent branches: LDS side effects are predicated through neutral operands.
 //  * Counter-based Philox streams (no RNG state in HBM) or injected draws (parity mode).
 #include <hip/hip_runtime.h>
 
 #include <mutex>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 
@@ -30,21 +37,35 @@ enum Policy { POL_EXTERNAL = 0, POL_GREEDY = 1, POL_RANDOM = 2 };
 enum Purpose : uint32_t { PUR_RESET = 1, PUR_REGEN = 2, PUR_POLICY = 3, PUR_RANDOM = 4 };
 constexpr int PH_ALL = 0, PH_PRE = 1, PH_REGEN = 2, PH_POLICY = 3;
 
+constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle agent
+constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
+
+// Shared (per-workgroup) table layout in bytes; built identically by build_tables() on the host.
+struct TableLayout {
+  int cell, rp, tag, dst, mv, valid, bytes;
+  __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
+      : cell(0), rp(32 * D), tag(32 * D + 4 * P), dst(32 * D + 8 * P), mv(32 * D + 8 * P + 4 * DP),
+        valid(32 * D + 8 * P + 4 * DP + 48), bytes(32 * D + 8 * P + 4 * DP + 48 + 4 * NV) {}
+};
+
 template <int D_, int R_, int NR_, int NAM_>
 struct Cfg {
   static constexpr int D = D_, R = R_, NR = NR_, NAM = NAM_;
   static constexpr int P = 4 * NR * NR;
   static constexpr int DP = 4 * (D - 4);
   static constexpr int PW = P / 4;
-  static constexpr int GRIDW = (D * D + 31) / 32;
   static constexpr int NV = (D - 2) * (D - 2) - P;      // interior cells that are not pickups
-  static constexpr int CELLB = (D * D + 3) & ~3;         // table bytes: cell -> pickup+1
-  static constexpr int TBL_BYTES = CELLB + 2 * P + 2 * NV;
-  static constexpr int TBLW = (TBL_BYTES + 3) / 4;
+  static constexpr TableLayout T = TableLayout(D, P, DP, NV);
+  static constexpr int TBLW = T.bytes / 4;
   static constexpr int L = 9 * R + 1;                    // observation row length
+  static_assert(D <= 32, "positions are 5-bit fields (occupancy rows are 32-bit words)");
   static_assert(P <= 64 && DP <= 64, "bitmask sets hold at most 64 points");
   static_assert(NAM <= R, "agents <= requests (core.py:89)");
 };
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
+__device__ __forceinline__ uint32_t as_u(short2v v) { return __builtin_bit_cast(uint32_t, v); }
 
 // ----------------------------------------------------------------------------- small helpers
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
@@ -117,17 +138,44 @@ __device__ __forceinline__ uint32_t nz_hi(uint32_t x) {
 }
 // 4 byte-flags (bit 7 of each byte) -> 4-bit nibble
 __device__ __forceinline__ uint32_t nib_of(uint32_t hi) { return ((hi >> 7) * 0x00204081u) >> 21 & 0xFu; }
-// 4-bit nibble -> 0xFF byte mask
+// 4-bit nibble -> 0xFF byte mask (full-rate 24-bit multiply)
 __device__ __forceinline__ uint32_t expand_nib(uint32_t nib) {
-  return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+  const uint32_t ones = __umul24(nib, 0x00204081u) & 0x01010101u;
+  return (ones << 8) - ones;
 }
 
+// packed i16 max/min, pinned: hipcc rewrites clamp(x, -1, 1) on i16 pairs into per-half
+// compare/select cascades (it recognises sign(x)); one v_pk_* op per bound is what we want.
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_min_i16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_min_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_sub_i16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_pk_sub_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// clamp(p + d) per 16-bit lane: the reference keeps the old coordinate when a +-1 move leaves
+// [0, D) (core.py:284-287), which for unit moves is exactly a clamp to [0, D-1].
 template <int D>
-__device__ __forceinline__ uint32_t delivery_xy(uint32_t d) {  // core.py:178-187
-  const uint32_t v = 2 + (d >> 2), side = d & 3u;
-  const uint32_t x = (side & 1u) ? (side == 3u ? (uint32_t)(D - 1) : 0u) : v;
-  const uint32_t y = (side & 1u) ? v : (side == 2u ? (uint32_t)(D - 1) : 0u);
-  return x | (y << 8);
+__device__ __forceinline__ uint32_t step16(uint32_t p, uint32_t d) {
+  short2v v = as_s2(p) + as_s2(d);
+  v = __builtin_elementwise_max(v, (short2v){0, 0});
+  v = __builtin_elementwise_min(v, (short2v){(short)(D - 1), (short)(D - 1)});
+  return as_u(v);
+}
+
+// action index of a unit step packed as (dx, dy) i16 pair: MOVES[a] = (a//3-1, a%3-1), core.py:38
+__device__ __forceinline__ uint32_t action_of(uint32_t d) {
+  const short2v v = as_s2(d);
+  return (uint32_t)(3 * ((int)v.x + 1) + ((int)v.y + 1));
 }
 
 template <class C>
@@ -136,32 +184,44 @@ struct Regs {
   uint32_t ag[C::NAM];
   uint32_t pt[C::PW];
   uint32_t pm[C::PW];
+  uint64_t am;   // open requests (derived from pt; kept in registers across fused steps)
 };
 
 template <class C>
 struct Lds {
   uint32_t tbl[C::TBLW];
-  uint32_t occ[C::GRIDW][BT];
-  uint32_t ptl[C::PW][BT];
-  uint32_t agl[C::NAM][BT];
-  __device__ __forceinline__ uint32_t cell_pickup(uint32_t cell) const {
-    return reinterpret_cast<const uint8_t*>(tbl)[cell];
+  uint32_t occ[C::D][BT];        // occupancy row y: bit x
+  uint32_t ptl[C::PW + 1][BT];   // pickup target bytes (+1 scratch word for predicated stores)
+  uint32_t agl[C::NAM][BT];      // agent words when processing in action-dict order
+  __device__ __forceinline__ uint32_t cell_pickup(uint32_t xy16) const {   // pickup index + 1 or 0
+    return reinterpret_cast<const uint8_t*>(tbl)[(xy16 & 31u) | (xy16 >> 11)];
   }
-  __device__ __forceinline__ uint32_t pickup_xy(uint32_t j) const {
-    return reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(tbl) + C::CELLB)[j];
-  }
-  __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const {
-    return reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(tbl) + C::CELLB +
-                                             2 * C::P)[v];
-  }
+  __device__ __forceinline__ uint32_t rp(uint32_t j) const { return tbl[C::T.rp / 4 + j]; }
+  __device__ __forceinline__ uint32_t tag(uint32_t j) const { return tbl[C::T.tag / 4 + j]; }
+  __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
+  __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
+  __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
   __device__ __forceinline__ uint8_t* ptl_byte(uint32_t j, int tid) {
     return reinterpret_cast<uint8_t*>(&ptl[j >> 2][tid]) + (j & 3u);
   }
 };
 
 template <class C>
-__device__ __forceinline__ void load_tables(Lds<C>& L, const uint32_t* __restrict__ tables) {
-  for (int w = threadIdx.x; w < C::TBLW; w += BT) L.tbl[w] = tables[w];
+__device__ __forceinline__ void load_tables(uint32_t* dst, const uint32_t* __restrict__ tables) {
+  for (int w = threadIdx.x; w < C::TBLW; w += BT) dst[w] = tables[w];
+}
+
+template <class C>
+__device__ __forceinline__ uint64_t active_mask(const Regs<C>& s) {
+  uint64_t am = 0;
+#pragma unroll
+  for (int w = 0; w < C::PW; ++w) am |= (uint64_t)nib_of(nz_hi(s.pt[w])) << (4 * w);
+  return am;
+}
+
+template <int N>
+__device__ __forceinline__ uint64_t low_mask() {
+  return N >= 64 ? ~0ull : ((1ull << N) - 1ull);
 }
 
 template <class C>
@@ -170,12 +230,13 @@ __device__ __forceinline__ void load_env(Regs<C>& s, const uint32_t* __restrict_
   s.hdr = st[e];
   s.epi = st[B + e];
 #pragma unroll
-  for (int i = 0; i < C::NAM; ++i) s.ag[i] = (i < na) ? st[(2 + i) * B + e] : 0u;
+  for (int i = 0; i < C::NAM; ++i) s.ag[i] = (i < na) ? st[(2 + i) * B + e] : IDLE;
   const int wpt = 2 + na;
 #pragma unroll
   for (int w = 0; w < C::PW; ++w) s.pt[w] = st[(wpt + w) * B + e];
 #pragma unroll
   for (int w = 0; w < C::PW; ++w) s.pm[w] = st[(wpt + C::PW + w) * B + e];
+  s.am = active_mask(s);
 }
 
 template <class C>
@@ -193,33 +254,21 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, uint32_t* __restrict
   for (int w = 0; w < C::PW; ++w) st[(wpt + C::PW + w) * B + e] = s.pm[w];
 }
 
-template <class C>
-__device__ __forceinline__ uint64_t active_mask(const Regs<C>& s) {
-  uint64_t am = 0;
-#pragma unroll
-  for (int w = 0; w < C::PW; ++w) am |= (uint64_t)nib_of(nz_hi(s.pt[w])) << (4 * w);
-  return am;
-}
-
-template <int N>
-__device__ __forceinline__ uint64_t low_mask() {
-  return N >= 64 ? ~0ull : ((1ull << N) - 1ull);
-}
-
 // ----------------------------------------------------------------------------- reset
 // core.py:167-221 (philox draws): spawn on interior non-pickup cells, open R requests.
 template <class C>
-__device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid, int na,
-                             int variable_n, uint32_t W, int tid) {
+__device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
+                                             int na, int variable_n, uint32_t W, int tid) {
   const uint32_t ep = s.epi + 1u;
   Reader rd(k, gid, ep, 0u, PUR_RESET);
   const uint32_t n = variable_n ? 1u + __umulhi(rd.word(0), (uint32_t)na) : (uint32_t)na;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) {
-    uint32_t a = 0;
+    uint32_t a = IDLE;
     if (i < na) {
       const uint32_t v = __umulhi(rd.word(1 + i), (uint32_t)C::NV);
-      a = (i < (int)n) ? L.valid_cell(v) : 0u;
+      const uint32_t cell = L.valid_cell(v);
+      a = (i < (int)n) ? (cell | IDLE) : IDLE;
     }
     s.ag[i] = a;
   }
@@ -242,22 +291,24 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
     s.pt[w] = L.ptl[w][tid];
     s.pm[w] = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu) & wb;
   }
+  s.am = opened;
   s.hdr = (n << 16) | (1u << 24);
   s.epi = ep;
 }
 
 template <class C>
-__device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e, int na, const int32_t* spawn,
-                               const int32_t* pickups, const int32_t* targets, const int32_t* nn,
-                               uint32_t W, int tid) {
+__device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e, int na,
+                                               const int32_t* spawn, const int32_t* pickups,
+                                               const int32_t* targets, const int32_t* nn,
+                                               uint32_t W, int tid) {
   const uint32_t n = nn ? min((uint32_t)nn[e], (uint32_t)na) : (uint32_t)na;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) {
-    uint32_t a = 0;
+    uint32_t a = IDLE;
     if (i < na && i < (int)n) {
       const uint32_t x = min((uint32_t)spawn[(e * na + i) * 2], (uint32_t)(C::D - 1));
       const uint32_t y = min((uint32_t)spawn[(e * na + i) * 2 + 1], (uint32_t)(C::D - 1));
-      a = x | (y << 8);
+      a = x | (y << 16) | IDLE;
     }
     s.ag[i] = a;
   }
@@ -277,17 +328,20 @@ __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e,
     s.pt[w] = L.ptl[w][tid];
     s.pm[w] = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu) & wb;
   }
+  s.am = opened;
   s.hdr = (n << 16) | (1u << 24);
   s.epi = s.epi + 1u;
 }
 
 // ----------------------------------------------------------------------------- policy
-// baseline/solvers.py:27-58 evaluated on the state: availability 0 (fresh reset or carrying)
-// -> head for the own delivery target (the null cell after reset), else for the nearest open
-// request by Manhattan distance, first (lowest pickup index) minimum wins; one step = clip(-1,1).
+// baseline/solvers.py:27-58 evaluated on the state, producing unit steps d (packed i16 pairs):
+// availability 0 (fresh reset, or carrying) -> head for the own delivery target (the null cell
+// after reset), else for the nearest open request by Manhattan distance, first (lowest pickup
+// index) minimum wins; step = clip(goal - pos, -1, 1).  Random actions come from the
+// POLICY/RANDOM streams.  Slots >= n stay (d = 0).
 template <class C, int POLICY>
-__device__ __forceinline__ void policy_actions(const Regs<C>& s, const Lds<C>& L, const Keys& k,
-                                               uint32_t gid, float p, uint32_t (&act)[C::NAM]) {
+__device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, const Keys& k,
+                                             uint32_t gid, float p, uint32_t (&d)[C::NAM]) {
   const uint32_t t = s.hdr & 0xFFFFu;
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   if (POLICY == POL_RANDOM) {
@@ -297,77 +351,73 @@ __device__ __forceinline__ void policy_actions(const Regs<C>& s, const Lds<C>& L
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int i = 4 * b + c;
-        if (i < C::NAM) act[i] = (i < (int)n) ? __umulhi(comp(blk, c), 9u) : 4u;
+        if (i < C::NAM) d[i] = L.mv(__umulhi(comp(blk, c), 9u));
       }
     }
-    return;
-  }
-  const bool fresh = (s.hdr >> 24) & 1u;
-  // open requests in ascending pickup order (core.py:409-418): tag = index << 16 | xy
-  uint32_t rtag[C::R];
-  uint64_t m = active_mask(s);
-#pragma unroll
-  for (int r = 0; r < C::R; ++r) {
-    const int j = m ? __builtin_ctzll(m) : 0;
-    rtag[r] = m ? (((uint32_t)j << 16) | L.pickup_xy((uint32_t)j)) : 0x00FFFFFFu;
-    m &= m - 1ull;
-  }
-  constexpr uint32_t null_xy = (uint32_t)(C::D / 2) | ((uint32_t)(C::D / 2) << 8);
-#pragma unroll
-  for (int i = 0; i < C::NAM; ++i) {
-    const uint32_t a = s.ag[i];
-    const uint32_t pos = a & 0xFFFFu;
-    const uint32_t carry = (a >> 16) & 0xFFu;
-    uint32_t best = 0xFFFFFFFFu;
+  } else {
+    asm volatile("; PHASE policy_rtag" ::: "memory");
+    const bool fresh = (s.hdr >> 24) & 1u;
+    // open requests in ascending pickup order (core.py:409-418)
+    uint32_t rp[C::R], tg[C::R];
+    uint64_t m = s.am;
 #pragma unroll
     for (int r = 0; r < C::R; ++r) {
-      const uint32_t d = __builtin_amdgcn_sad_u8(pos, rtag[r] & 0xFFFFu, 0u);
-      best = min(best, (d << 24) | rtag[r]);
+      const bool has = m != 0ull;
+      const uint32_t j = has ? (uint32_t)__builtin_ctzll(m) : 0u;
+      const uint32_t a = L.rp(j), b = L.tag(j);
+      rp[r] = has ? a : XY16;           // a far-away cell: never the minimum
+      tg[r] = has ? b : 0xFFFFu;
+      m &= m - 1ull;
     }
-    uint32_t goal = best & 0xFFFFu;
-    if (carry) goal = delivery_xy<C::D>(carry - 1u);
-    if (fresh) goal = null_xy;
-    const int x = (int)(pos & 0xFFu), y = (int)(pos >> 8);
-    const int gx = (int)(goal & 0xFFu), gy = (int)(goal >> 8);
-    const int sx = (gx > x) - (gx < x), sy = (gy > y) - (gy < y);
-    act[i] = (uint32_t)((sx + 1) * 3 + (sy + 1));
-  }
-  if (p > 0.0f) {
+    asm volatile("; PHASE policy_agents" ::: "memory");
+    constexpr uint32_t null16 = (uint32_t)(C::D / 2) | ((uint32_t)(C::D / 2) << 16);
 #pragma unroll
-    for (int b = 0; b < (C::NAM + 1) / 2; ++b) {
-      const uint4 blk = stream_block(k, gid, s.epi, t, PUR_POLICY, (uint32_t)b);
+    for (int i = 0; i < C::NAM; ++i) {
+      const uint32_t a = s.ag[i];
+      const uint32_t pos = a & XY16;
+      uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = 2 * b + h;
-        if (i < C::NAM) {
-          const float u = (float)(comp(blk, 2 * h) >> 8) * (1.0f / 16777216.0f);
-          if (u < p) act[i] = __umulhi(comp(blk, 2 * h + 1), 9u);
+      for (int r = 0; r < C::R; ++r)   // key = dist << 16 | pickup << 10 | x << 5 | y
+        best = min(best, __builtin_amdgcn_sad_hi_u8(pos, rp[r], tg[r]));
+      const uint32_t near = ((best >> 5) & 31u) | ((best & 31u) << 16);
+      const uint32_t dst = (a >> 8) & XY16;
+      const bool carrying = (a & 0xFF00u) != 0xFF00u;
+      uint32_t goal = carrying ? dst : near;
+      goal = fresh ? null16 : goal;
+      d[i] = pk_min_i16(pk_max_i16(pk_sub_i16(goal, pos), 0xFFFFFFFFu), 0x00010001u);
+    }
+    if (p > 0.0f) {
+#pragma unroll
+      for (int b = 0; b < (C::NAM + 1) / 2; ++b) {
+        const uint4 blk = stream_block(k, gid, s.epi, t, PUR_POLICY, (uint32_t)b);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * b + h;
+          if (i < C::NAM) {
+            const float u = (float)(comp(blk, 2 * h) >> 8) * (1.0f / 16777216.0f);
+            const uint32_t rnd = L.mv(__umulhi(comp(blk, 2 * h + 1), 9u));
+            d[i] = (u < p) ? rnd : d[i];
+          }
         }
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < C::NAM; ++i)
-    if (i >= (int)n) act[i] = 4u;
+  for (int i = 0; i < C::NAM; ++i) d[i] = (i < (int)n) ? d[i] : 0u;
 }
 
 // ----------------------------------------------------------------------------- step
-struct StepOut {
-  float* rewards;
-  uint8_t* dones;
-  int32_t* n_inactive;
-};
-
-// core.py:267-368 on one env held in registers.  Returns done.
+// core.py:267-368 on one env held in registers.  Returns done.  No data-dependent branches:
+// LDS side effects are predicated through neutral operands (and ~0 / or 0 / the scratch word),
+// so each phase is one basic block and its LDS reads issue back to back.
 template <class C>
-__device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&act)[C::NAM],
+__device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
                                          const int32_t* __restrict__ actions_g,
                                          const int32_t* __restrict__ regen, const Keys& k,
                                          uint32_t gid, int64_t e, int na, int phase, uint32_t T,
                                          uint32_t W, float (&rew)[C::NAM], int32_t* n_inactive,
-                                         int tid) {
-  constexpr int D = C::D;
+                                         int tid, int ablate) {
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   uint32_t t = s.hdr & 0xFFFFu;
 
@@ -377,170 +427,184 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     for (int i = 0; i < C::NAM; ++i) rew[i] = 0.0f;
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
+    asm volatile("; PHASE move" ::: "memory");
+    if (!(ablate & 2)) {
 #pragma unroll
-    for (int w = 0; w < C::GRIDW; ++w) L.occ[w][tid] = 0u;
+      for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
 #pragma unroll
-    for (int i = 0; i < C::NAM; ++i) {
-      if (i < (int)n) {
-        const uint32_t c = (s.ag[i] & 0xFFu) * D + ((s.ag[i] >> 8) & 0xFFu);
-        atomicOr(&L.occ[c >> 5][tid], 1u << (c & 31u));
+      for (int i = 0; i < C::NAM; ++i) {
+        const uint32_t p = s.ag[i] & XY16;
+        atomicOr(&L.occ[p >> 16][tid], (i < (int)n) ? (1u << (p & 31u)) : 0u);
       }
-    }
-    const bool ordered = order != nullptr;
-    if (ordered) {
-#pragma unroll
-      for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
-    }
-    uint32_t kk[3 * C::NAM];
-#pragma unroll
-    for (int j = 0; j < 3 * C::NAM; ++j) kk[j] = 0xFFFFFFFFu;
-#pragma unroll
-    for (int sidx = 0; sidx < C::NAM; ++sidx) {
-      bool live;
-      uint32_t a, mv;
-      int who = sidx;
+      const bool ordered = order != nullptr;
       if (ordered) {
-        who = (sidx < na) ? order[e * na + sidx] : -1;
-        live = who >= 0 && who < (int)n && who < C::NAM;
-        who = live ? who : 0;
-        a = L.agl[who][tid];
-        mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
-      } else {
-        live = sidx < (int)n;
-        a = s.ag[sidx];
-        mv = act[sidx];
-      }
-      mv = mv > 8u ? 4u : mv;
-      const int px = (int)(a & 0xFFu), py = (int)((a >> 8) & 0xFFu);
-      const int q = (int)((mv * 11u) >> 5);                 // mv / 3 for mv <= 8
-      int x = px + q - 1, y = py + (int)mv - 3 * q - 1;     // MOVES[a] = (a//3-1, a%3-1)
-      if ((unsigned)x >= (unsigned)D) x = px;
-      if ((unsigned)y >= (unsigned)D) y = py;
-      const uint32_t cn = (uint32_t)(x * D + y);
-      const bool occupied = (L.occ[cn >> 5][tid] >> (cn & 31u)) & 1u;
-      const uint32_t key = (uint32_t)px | ((uint32_t)py << 8) | ((uint32_t)x << 16) | ((uint32_t)y << 24);
-      bool forbidden = false;
 #pragma unroll
-      for (int j = 0; j < 3 * sidx; ++j) forbidden |= (kk[j] == key);
-      if (live && !occupied && !forbidden) {
-        const uint32_t co = (uint32_t)(px * D + py);
-        atomicAnd(&L.occ[co >> 5][tid], ~(1u << (co & 31u)));
-        atomicOr(&L.occ[cn >> 5][tid], 1u << (cn & 31u));
-        kk[3 * sidx] = (uint32_t)x | ((uint32_t)y << 8) | ((uint32_t)px << 16) | ((uint32_t)py << 24);
-        if (x != px && y != py) {
-          kk[3 * sidx + 1] = (uint32_t)x | ((uint32_t)py << 8) | ((uint32_t)px << 16) | ((uint32_t)y << 24);
-          kk[3 * sidx + 2] = (uint32_t)px | ((uint32_t)y << 8) | ((uint32_t)x << 16) | ((uint32_t)py << 24);
+        for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
+      }
+      // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
+      uint32_t kk[3 * C::NAM];
+#pragma unroll
+      for (int sidx = 0; sidx < C::NAM; ++sidx) {
+        bool live;
+        uint32_t a, dd;
+        int who = sidx;
+        if (ordered) {
+          who = (sidx < na) ? order[e * na + sidx] : -1;
+          live = who >= 0 && who < (int)n && who < C::NAM;
+          who = live ? who : 0;
+          a = L.agl[who][tid];
+          const uint32_t mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
+          dd = L.mv(mv > 8u ? 4u : mv);
+        } else {
+          live = sidx < (int)n;
+          a = s.ag[sidx];
+          dd = dstep[sidx];
         }
-        const uint32_t na_ = (a & 0xFFFF0000u) | (uint32_t)x | ((uint32_t)y << 8);
-        if (ordered)
-          L.agl[who][tid] = na_;
-        else
-          s.ag[sidx] = na_;
-      }
-    }
-    if (ordered) {
+        const uint32_t p = a & XY16;
+        const uint32_t c = step16<C::D>(p, dd);
+        const bool occupied = (L.occ[c >> 16][tid] >> (c & 31u)) & 1u;
+        const uint32_t key = p | (c << 8);
+        uint32_t f = 0xFFFFFFFFu;
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) s.ag[i] = L.agl[i][tid];
+        for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
+        const bool ok = live && !occupied && f != 0u;
+        atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
+        atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
+        const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u);   // (x, py)
+        const uint32_t c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);   // (px, y)
+        const uint32_t dx = c ^ p;
+        const bool diag = ok && (dx & 0xFFFFu) && (dx >> 16);
+        kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
+        kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
+        kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
+        const uint32_t moved = ok ? ((a & ~XY16) | c) : a;
+        if (ordered)
+          L.agl[who][tid] = moved;
+        else
+          s.ag[sidx] = moved;
+      }
+      if (ordered) {
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) s.ag[i] = L.agl[i][tid];
+      }
     }
 
     // ---- request expiry (core.py:303-306), 4 pickup points per op
+    asm volatile("; PHASE expire" ::: "memory");
+    if (!(ablate & 4)) {
+      uint32_t any_exp = 0;
 #pragma unroll
-    for (int w = 0; w < C::PW; ++w) {
-      const uint32_t live = nz_hi(s.pt[w]);
-      uint32_t tm = s.pm[w] - (live >> 7);
-      const uint32_t zero = ~((((tm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tm)) & 0x80808080u;
-      const uint32_t m = ((zero & live) >> 7) * 0xFFu;
-      s.pt[w] &= ~m;
-      s.pm[w] = tm & ~m;
+      for (int w = 0; w < C::PW; ++w) {
+        const uint32_t live = nz_hi(s.pt[w]);
+        const uint32_t tm = s.pm[w] - (live >> 7);
+        const uint32_t zero = ~((((tm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tm)) & 0x80808080u;
+        const uint32_t ex = zero & live;
+        const uint32_t m = (ex >> 7) * 0xFFu;
+        any_exp |= ex;
+        s.pt[w] &= ~m;
+        s.pm[w] = tm & ~m;
+      }
+      if (__any(any_exp != 0u)) s.am = active_mask(s);   // rare: only reset-time requests expire
     }
 
     // ---- pickups: gather for every agent against the pre-pickup table, then clear
     //      (core.py:309-335; two agents on one point both pick it up)
+    asm volatile("; PHASE pickup" ::: "memory");
+    if (!(ablate & 8)) {
 #pragma unroll
-    for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
-    uint64_t picked = 0;
+      for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
+      uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];
 #pragma unroll
-    for (int i = 0; i < C::NAM; ++i) {
-      const uint32_t a = s.ag[i];
-      const uint32_t cell = (a & 0xFFu) * D + ((a >> 8) & 0xFFu);
-      const uint32_t cp = L.cell_pickup(cell);
-      if (i < (int)n && cp != 0u && ((a >> 16) & 0xFFu) == 0u) {
-        const uint32_t tg = *L.ptl_byte(cp - 1u, tid);
-        if (tg) {
-          s.ag[i] = a | (tg << 16);
-          picked |= 1ull << (cp - 1u);
-          rew[i] = 1.0f;
-        }
+      for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(cp[i] ? cp[i] - 1u : 0u, tid);
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
+      uint64_t picked = 0;
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) {
+        const uint32_t a = s.ag[i];
+        const bool take = (i < (int)n) & (cp[i] != 0u) & ((a & 0xFF00u) == 0xFF00u) & (tb[i] != 0u);
+        s.ag[i] = take ? ((a & XY16) | (dst[i] << 8)) : a;
+        picked |= take ? (1ull << ((cp[i] - 1u) & 63u)) : 0ull;
+        rew[i] = take ? 1.0f : 0.0f;
       }
-    }
 #pragma unroll
-    for (int w = 0; w < C::PW; ++w) {
-      const uint32_t m = expand_nib((uint32_t)(picked >> (4 * w)) & 0xFu);
-      s.pt[w] &= ~m;
-      s.pm[w] &= ~m;
+      for (int w = 0; w < C::PW; ++w) {
+        const uint32_t m = expand_nib((uint32_t)(picked >> (4 * w)) & 0xFu);
+        s.pt[w] &= ~m;
+        s.pm[w] &= ~m;
+      }
+      s.am &= ~picked;
     }
   }
 
   // ---- regeneration: reopen k = R - P + |inactive| points (core.py:338-351)
-  {
-    const uint64_t inactive = ~active_mask(s) & low_mask<C::P>();
+  asm volatile("; PHASE regen" ::: "memory");
+  if (!(ablate & 16)) {
+    const uint64_t inactive = ~s.am & low_mask<C::P>();
     const uint32_t nin = (uint32_t)__popcll(inactive);
     const int kreq = C::R - C::P + (int)nin;
     if (phase == PH_PRE) {
       if (n_inactive) n_inactive[e] = (int32_t)nin;
     } else {
       uint64_t rem = inactive, used = 0, opened = 0;
-      const uint32_t tnew = t;
+      uint32_t first_t = 0;
       uint4 blk = make_uint4(0u, 0u, 0u, 0u);   // words 2j (pickup) and 2j+1 (target) share a block
 #pragma unroll
       for (int j = 0; j < C::R; ++j) {
-        if (j < kreq) {
-          int sel, tg;
+        if (__any(j < kreq)) {                  // wave-uniform: skip items no env needs
+          const bool act_j = j < kreq;
+          int sel, tgi;
           if (regen) {
-            const uint32_t rp = (uint32_t)regen[e * 2 * C::R + j];
-            sel = rp < nin ? select_bit64(inactive, rp) : C::P;       // out-of-range draw: ignored
-            tg = regen[e * 2 * C::R + C::R + j];
-            if ((uint32_t)tg >= (uint32_t)C::DP) sel = C::P;
+            const uint32_t rpos = act_j ? (uint32_t)regen[e * 2 * C::R + j] : 0u;
+            tgi = act_j ? regen[e * 2 * C::R + C::R + j] : 0;
+            sel = (rpos < nin && (uint32_t)tgi < (uint32_t)C::DP) ? select_bit64(inactive, rpos) : C::P;
           } else {
-            if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, tnew, PUR_REGEN, (uint32_t)(j >> 1));
+            if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
             const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
             sel = select_bit64(rem, __umulhi(w1, nin - (uint32_t)j));
-            rem &= ~(1ull << sel);
-            tg = select_bit64(~used & low_mask<C::DP>(), __umulhi(w2, (uint32_t)(C::DP - j)));
-            used |= 1ull << tg;
+            const uint32_t r2 = __umulhi(w2, (uint32_t)(C::DP - j));
+            if (j == 0) tgi = (int)r2;                                   // nothing used yet
+            else if (j == 1) tgi = (int)(r2 + (r2 >= first_t ? 1u : 0u));  // one point removed
+            else tgi = select_bit64(~used & low_mask<C::DP>(), r2);
+            if (j == 0) first_t = r2;
           }
-          if (sel < C::P) {
-            opened |= 1ull << sel;
-            *L.ptl_byte((uint32_t)sel, tid) = (uint8_t)(tg + 1);
-          }
+          const bool apply = act_j && sel < C::P;
+          rem &= apply ? ~(1ull << (sel & 63)) : ~0ull;
+          used |= apply ? (1ull << (tgi & 63)) : 0ull;
+          opened |= apply ? (1ull << (sel & 63)) : 0ull;
+          // predicated byte store: inactive lanes write the scratch word
+          *L.ptl_byte(apply ? (uint32_t)sel : (uint32_t)(4 * C::PW), tid) = (uint8_t)(tgi + 1);
         }
       }
-      if (opened) {
+      if (__any(opened != 0ull)) {
         const uint32_t wb = W * 0x01010101u;
 #pragma unroll
         for (int w = 0; w < C::PW; ++w) {
           const uint32_t m = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu);
-          if (m) {
-            s.pt[w] = (s.pt[w] & ~m) | (L.ptl[w][tid] & m);
-            s.pm[w] = (s.pm[w] & ~m) | (wb & m);
-          }
+          s.pt[w] = (s.pt[w] & ~m) | (L.ptl[w][tid] & m);
+          s.pm[w] = (s.pm[w] & ~m) | (wb & m);
         }
       }
+      s.am |= opened;
     }
   }
 
   bool done = false;
   if (phase != PH_REGEN) {
-    // ---- deliveries (core.py:354-368)
+    // ---- deliveries (core.py:354-368): target cell == position (idle agents never match)
+    asm volatile("; PHASE deliver" ::: "memory");
+    if (!(ablate & 32)) {
 #pragma unroll
-    for (int i = 0; i < C::NAM; ++i) {
-      const uint32_t a = s.ag[i];
-      const uint32_t carry = (a >> 16) & 0xFFu;
-      if (carry && delivery_xy<C::D>(carry - 1u) == (a & 0xFFFFu)) {
-        s.ag[i] = a & 0xFF00FFFFu;
-        rew[i] += 1.0f;
+      for (int i = 0; i < C::NAM; ++i) {
+        const uint32_t a = s.ag[i];
+        const bool arrived = ((a >> 8) & XY16) == (a & XY16);
+        s.ag[i] = arrived ? (a | IDLE) : a;
+        rew[i] += arrived ? 1.0f : 0.0f;
       }
     }
+    asm volatile("; PHASE tail" ::: "memory");
     done = t >= T;                                            // core.py:438
     s.hdr = t | (n << 16);                                    // clears `fresh`
   }
@@ -548,6 +612,45 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 }
 
 // ----------------------------------------------------------------------------- kernels
+// rewards[B, na]: a wave's 64 envs own one contiguous block of 64*na floats.  Lanes write their
+// rows into LDS (the agl scratch, free after the move phase) and read the block back so every
+// global store instruction writes contiguous 16-byte lanes (1 KiB per wave-instruction) instead
+// of one strided row per lane.
+template <class C>
+__device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::NAM], float* out,
+                                              int64_t B, int64_t e, int na, int tid) {
+  const int lane = tid & 63;
+  const int64_t e0 = e - lane;
+  if (B - e0 < 64) {   // tail wave: lanes past B have exited, so no transpose -- one row per lane
+    float* row = out + e * na;
+#pragma unroll
+    for (int i = 0; i < C::NAM; ++i)
+      if (i < na) row[i] = rew[i];
+    return;
+  }
+  float* stg = reinterpret_cast<float*>(&L.agl[0][0]) + (tid >> 6) * 64 * C::NAM;
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i)
+    if (i < na) stg[lane * na + i] = rew[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nvalid = 64 * na;
+  float* wout = out + e0 * na;
+  if ((reinterpret_cast<uintptr_t>(wout) & 15u) == 0 && (na & 3) == 0) {
+#pragma unroll
+    for (int q = 0; q < C::NAM / 4; ++q)
+      if (4 * q < na)
+        reinterpret_cast<float4*>(wout)[lane + 64 * q] = reinterpret_cast<const float4*>(stg)[lane + 64 * q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < C::NAM; ++q)
+      if (lane + 64 * q < nvalid) wout[lane + 64 * q] = stg[lane + 64 * q];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 struct StepParams {
   uint32_t* state;
   int64_t B;
@@ -565,12 +668,13 @@ struct StepParams {
   uint32_t k0, k1;
   int64_t env_offset;
   int32_t steps, phase, autoreset, variable_n;
+  int32_t ablate;  // timing-only phase skips (env WH_ABLATE), never set in normal use
 };
 
 template <class C, int POLICY>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
-  load_tables<C>(L, a.tables);
+  load_tables<C>(L.tbl, a.tables);
   __syncthreads();
   const int tid = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
@@ -581,34 +685,36 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   load_env<C>(s, a.state, a.B, e, a.na);
 
   if (a.phase == PH_POLICY) {
-    uint32_t act[C::NAM];
-    policy_actions<C, POLICY>(s, L, k, gid, a.p, act);
+    uint32_t d[C::NAM];
+    policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+    const uint32_t n = (s.hdr >> 16) & 0xFFu;
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i)
-      if (i < a.na) a.actions_out[e * a.na + i] = (int32_t)act[i];
+      if (i < a.na) a.actions_out[e * a.na + i] = (i < (int)n) ? (int32_t)action_of(d[i]) : 4;
     return;
   }
 
   float ret = 0.0f;
   for (int stp = 0; stp < a.steps; ++stp) {
-    uint32_t act[C::NAM];
+    uint32_t d[C::NAM];
     if (POLICY == POL_EXTERNAL) {
       const bool have = a.phase != PH_REGEN && a.order == nullptr;   // REGEN reads no actions
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) act[i] = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
+      for (int i = 0; i < C::NAM; ++i) {
+        uint32_t mv = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
+        d[i] = L.mv(mv > 8u ? 4u : mv);
+      }
+    } else if (a.ablate & 1) {
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
     } else {
-      policy_actions<C, POLICY>(s, L, k, gid, a.p, act);
+      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C>(s, L, act, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
-                                  (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid);
+    const bool done = step_env<C>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
+                                  (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, a.ablate);
     if (a.phase != PH_REGEN) {
-      if (a.rewards) {
-        float* rp = a.rewards + ((int64_t)stp * a.B + e) * a.na;
-#pragma unroll
-        for (int i = 0; i < C::NAM; ++i)
-          if (i < a.na) rp[i] = rew[i];
-      }
+      if (a.rewards) store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid);
       if (a.dones) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
       if (a.returns) {
 #pragma unroll
@@ -636,7 +742,7 @@ struct ResetParams {
 template <class C>
 __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
   __shared__ Lds<C> L;
-  load_tables<C>(L, a.tables);
+  load_tables<C>(L.tbl, a.tables);
   __syncthreads();
   const int tid = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
@@ -664,6 +770,7 @@ struct ObsLds {
   uint8_t img[OBS_EB][IMG];
   uint8_t fresh[OBS_EB];
   uint32_t desc[C::L];
+  uint32_t tbl[C::TBLW];
 };
 
 template <class C>
@@ -671,11 +778,10 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
                                                 const uint32_t* __restrict__ tables,
                                                 float* __restrict__ obs) {
   __shared__ ObsLds<C> O;
-  __shared__ uint32_t tbl[C::TBLW];
   constexpr int R = C::R, D = C::D;
   constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
   const int tid = threadIdx.x;
-  for (int w = tid; w < C::TBLW; w += BT) tbl[w] = tables[w];
+  load_tables<C>(O.tbl, tables);
   // feature descriptors: base | stride << 10 | mode << 14 | j << 16
   //   mode 0: fixed byte; 1: other row skip i; 2: other row skip (fresh ? i : 1); 3: own row
   for (int f = tid; f < C::L; f += BT) {
@@ -701,16 +807,15 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
     const uint8_t nul = (uint8_t)(D / 2);
     im[0] = (uint8_t)n;
     for (int r = 0; r < R; ++r) {
-      uint32_t a = (r < na && r < (int)n) ? state[(2 + r) * B + e] : 0u;
-      const bool live = r < (int)n;
-      const uint32_t carry = (a >> 16) & 0xFFu;
+      const bool live = r < (int)n && r < na;
+      const uint32_t a = live ? state[(2 + r) * B + e] : IDLE;
+      const bool carry = (a & 0xFF00u) != 0xFF00u;
       im[A0 + r] = (uint8_t)((live && !fresh && !carry) ? 1 : 0);
-      uint32_t dxy = (uint32_t)nul | ((uint32_t)nul << 8);
-      if (live && !fresh && carry) dxy = delivery_xy<D>(carry - 1u);
-      im[G0 + 2 * r] = (uint8_t)(dxy & 0xFFu);
-      im[G0 + 2 * r + 1] = (uint8_t)(dxy >> 8);
+      const bool show = live && !fresh && carry;
+      im[G0 + 2 * r] = show ? (uint8_t)((a >> 8) & 0xFFu) : nul;
+      im[G0 + 2 * r + 1] = show ? (uint8_t)(a >> 24) : nul;
       im[P0 + 2 * r] = live ? (uint8_t)(a & 0xFFu) : nul;
-      im[P0 + 2 * r + 1] = live ? (uint8_t)((a >> 8) & 0xFFu) : nul;
+      im[P0 + 2 * r + 1] = live ? (uint8_t)((a >> 16) & 0xFFu) : nul;
     }
     const int wpt = 2 + na;
     int r = 0;
@@ -719,13 +824,12 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
       for (int b = 0; b < 4; ++b) {
         const uint32_t tg = (pt >> (8 * b)) & 0xFFu;
         if (tg && r < R) {
-          const uint32_t j = 4u * w + b;
-          const uint32_t pxy = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(tbl) + C::CELLB)[j];
-          const uint32_t dxy = delivery_xy<D>(tg - 1u);
+          const uint32_t pxy = O.tbl[C::T.rp / 4 + 4 * w + b];
+          const uint32_t dxy = O.tbl[C::T.dst / 4 + ((tg - 1u) & 63u)];
           im[Q0 + 4 * r] = (uint8_t)(pxy & 0xFFu);
-          im[Q0 + 4 * r + 1] = (uint8_t)(pxy >> 8);
+          im[Q0 + 4 * r + 1] = (uint8_t)(pxy >> 16);
           im[Q0 + 4 * r + 2] = (uint8_t)(dxy & 0xFFu);
-          im[Q0 + 4 * r + 3] = (uint8_t)(dxy >> 8);
+          im[Q0 + 4 * r + 3] = (uint8_t)(dxy >> 16);
           ++r;
         }
       }
@@ -764,6 +868,20 @@ struct PackParams {
   uint32_t* episode;
 };
 
+// delivery index -> (x, y) and back (core.py:177-188)
+__device__ __forceinline__ uint32_t delivery_cell(int32_t d, int D) {
+  const uint32_t v = 2 + ((uint32_t)d >> 2), side = (uint32_t)d & 3u;
+  const uint32_t x = (side & 1u) ? (side == 3u ? (uint32_t)(D - 1) : 0u) : v;
+  const uint32_t y = (side & 1u) ? v : (side == 2u ? (uint32_t)(D - 1) : 0u);
+  return x | (y << 16);
+}
+__device__ __forceinline__ int32_t delivery_index(uint32_t x, uint32_t y, int D) {
+  if (y == 0) return 4 * ((int32_t)x - 2);
+  if (x == 0) return 4 * ((int32_t)y - 2) + 1;
+  if (y == (uint32_t)(D - 1)) return 4 * ((int32_t)x - 2) + 2;
+  return 4 * ((int32_t)y - 2) + 3;
+}
+
 __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
   const int64_t e = (int64_t)blockIdx.x * BT + threadIdx.x;
   if (e >= a.B) return;
@@ -772,13 +890,14 @@ __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
   const uint32_t n = min((uint32_t)max(a.n[e], 0), (uint32_t)a.na);
   a.state[e] = ((uint32_t)a.t[e] & 0xFFFFu) | (n << 16) | (a.fresh[e] ? (1u << 24) : 0u);
   a.state[B + e] = a.episode[e];
+  const int32_t DP = 4 * (a.D - 4);
   for (int i = 0; i < a.na; ++i) {
-    uint32_t w = 0;
+    uint32_t w = IDLE;
     if (i < (int)n) {
       const int32_t tg = a.agent_target[e * a.na + i];
       const uint32_t x = (uint32_t)min(max(a.pos[(e * a.na + i) * 2], 0), a.D - 1);
       const uint32_t y = (uint32_t)min(max(a.pos[(e * a.na + i) * 2 + 1], 0), a.D - 1);
-      w = x | (y << 8) | ((uint32_t)min(max(tg + 1, 0), 255) << 16);
+      w = x | (y << 16) | ((tg >= 0 && tg < DP) ? (delivery_cell(tg, a.D) << 8) : IDLE);
     }
     a.state[(2 + i) * B + e] = w;
   }
@@ -787,8 +906,8 @@ __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
     for (int b = 0; b < 4; ++b) {
       const int j = 4 * w + b;
       const int32_t tg = a.pickup_target[e * a.P + j];
-      if (tg >= 0) {
-        tw |= (uint32_t)min(tg + 1, 255) << (8 * b);
+      if (tg >= 0 && tg < DP) {
+        tw |= (uint32_t)(tg + 1) << (8 * b);
         mw |= ((uint32_t)a.pickup_timer[e * a.P + j] & 0xFFu) << (8 * b);
       }
     }
@@ -809,9 +928,11 @@ __global__ __launch_bounds__(BT) void k_unpack(PackParams a) {
   a.episode[e] = a.cstate[B + e];
   for (int i = 0; i < a.na; ++i) {
     const uint32_t w = a.cstate[(2 + i) * B + e];
-    a.pos[(e * a.na + i) * 2] = (int32_t)(w & 0xFFu);
-    a.pos[(e * a.na + i) * 2 + 1] = (int32_t)((w >> 8) & 0xFFu);
-    a.agent_target[e * a.na + i] = (int32_t)((w >> 16) & 0xFFu) - 1;
+    const bool live = i < (int)n;
+    a.pos[(e * a.na + i) * 2] = live ? (int32_t)(w & 0xFFu) : 0;
+    a.pos[(e * a.na + i) * 2 + 1] = live ? (int32_t)((w >> 16) & 0xFFu) : 0;
+    const bool carry = live && (w & 0xFF00u) != 0xFF00u;
+    a.agent_target[e * a.na + i] = carry ? delivery_index((w >> 8) & 0xFFu, w >> 24, a.D) : -1;
   }
   for (int w = 0; w < a.pw; ++w) {
     const uint32_t tw = a.cstate[(2 + a.na + w) * B + e];
@@ -841,7 +962,7 @@ int validate(const wh_config* c, Geometry* g) {
   g->NA = c->agent_slots;
   g->T = c->episode_duration;
   g->W = c->pickup_wait_duration;
-  if (g->NR < 1 || g->NR > WH_MAX_RACKS || g->D < 5 || g->D > 255) return WH_EINVAL;
+  if (g->NR < 1 || g->NR > WH_MAX_RACKS || g->D < 5 || g->D > 32) return WH_EINVAL;
   g->P = 4 * g->NR * g->NR;
   g->DP = 4 * (g->D - 4);
   if (g->NA < 1 || g->NA > g->R || g->R > g->P || g->R > g->DP) return WH_EINVAL;
@@ -853,31 +974,52 @@ int validate(const wh_config* c, Geometry* g) {
   return WH_OK;
 }
 
-// host tables: cell -> pickup + 1, pickup xy, valid spawn cells (core.py:170-199)
+// Host copy of the per-workgroup tables, same layout as TableLayout (core.py:170-199):
+//   cell  [32*D] u8  : (x | y << 5) -> pickup index + 1, 0 = not a pickup cell
+//   rp    [P]    u32 : pickup cell as x | y << 16
+//   tag   [P]    u32 : pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58)
+//   dst   [Dp]   u32 : delivery cell as x | y << 16
+//   mv    [12]   u32 : MOVES[a] as packed i16 (dx, dy) (core.py:38)
+//   valid [NV]   u32 : interior non-pickup cells x | y << 16, ascending (x, y) (spawn, core.py:191-199)
 std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
-  const int cellb = (g.D * g.D + 3) & ~3;
-  std::vector<uint8_t> cell(cellb, 0);
-  std::vector<uint16_t> pxy(g.P);
+  const int D = g.D;
   *bad = 0;
+  if (D > 32) { *bad = 1; return {}; }
+  std::vector<uint8_t> cell(32 * D, 0);
+  std::vector<uint32_t> rp(g.P), tag(g.P);
   for (int ix = 0; ix < g.NR; ++ix)
     for (int iy = 0; iy < g.NR; ++iy)
       for (int q = 0; q < 4; ++q) {
         const int j = (ix * g.NR + iy) * 4 + q;
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
-        if (cell[x * g.D + y]) *bad = 1;  // overlapping racks
-        cell[x * g.D + y] = (uint8_t)(j + 1);
-        pxy[j] = (uint16_t)(x | (y << 8));
+        if (cell[x | (y << 5)]) *bad = 1;  // overlapping racks
+        cell[x | (y << 5)] = (uint8_t)(j + 1);
+        rp[j] = (uint32_t)x | ((uint32_t)y << 16);
+        tag[j] = ((uint32_t)j << 10) | ((uint32_t)x << 5) | (uint32_t)y;
       }
-  std::vector<uint16_t> valid;
-  for (int x = 1; x < g.D - 1; ++x)
-    for (int y = 1; y < g.D - 1; ++y)
-      if (!cell[x * g.D + y]) valid.push_back((uint16_t)(x | (y << 8)));
-  std::vector<uint8_t> bytes(cell);
-  for (uint16_t v : pxy) { bytes.push_back(v & 0xFF); bytes.push_back(v >> 8); }
-  for (uint16_t v : valid) { bytes.push_back(v & 0xFF); bytes.push_back(v >> 8); }
-  while (bytes.size() % 4) bytes.push_back(0);
-  std::vector<uint32_t> words(bytes.size() / 4);
-  memcpy(words.data(), bytes.data(), bytes.size());
+  std::vector<uint32_t> dst(g.DP);
+  for (int d = 0; d < g.DP; ++d) {
+    const int v = 2 + d / 4, side = d % 4;
+    const int x = (side & 1) ? (side == 3 ? D - 1 : 0) : v;
+    const int y = (side & 1) ? v : (side == 2 ? D - 1 : 0);
+    dst[d] = (uint32_t)x | ((uint32_t)y << 16);
+  }
+  std::vector<uint32_t> mv(12, 0);
+  for (int a = 0; a < 9; ++a) {
+    const int dx = a / 3 - 1, dy = a % 3 - 1;
+    mv[a] = (uint32_t)(uint16_t)(int16_t)dx | ((uint32_t)(uint16_t)(int16_t)dy << 16);
+  }
+  std::vector<uint32_t> valid;
+  for (int x = 1; x < D - 1; ++x)
+    for (int y = 1; y < D - 1; ++y)
+      if (!cell[x | (y << 5)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
+  std::vector<uint32_t> words((cell.size() + 3) / 4, 0);
+  memcpy(words.data(), cell.data(), cell.size());
+  words.insert(words.end(), rp.begin(), rp.end());
+  words.insert(words.end(), tag.begin(), tag.end());
+  words.insert(words.end(), dst.begin(), dst.end());
+  words.insert(words.end(), mv.begin(), mv.end());
+  words.insert(words.end(), valid.begin(), valid.end());
   return words;
 }
 
@@ -977,7 +1119,7 @@ inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + BT - 1) / BT)); }
 // =============================================================================== C ABI
 extern "C" {
 
-const char* wh_version(void) { return "warehouse_amd gfx950 lane-per-env v1 " __DATE__; }
+const char* wh_version(void) { return "warehouse_amd gfx950 lane-per-env v2 " __DATE__; }
 
 int wh_query(const wh_config* cfg, wh_layout* out) {
   Geometry g;
@@ -1066,6 +1208,8 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   a.T = g.T;
   a.W = g.W;
   a.tables = tab;
+  const char* abl = getenv("WH_ABLATE");   // timing experiments only (tools/ablate.py)
+  a.ablate = abl ? atoi(abl) : 0;
   hipLaunchKernelGGL(k->step[policy], grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());
 }

@@ -1,0 +1,32 @@
+"""Phase-ablation timing of the fused step kernel (timing only: results are wrong by design).
+WH_ABLATE bits: 1 policy, 2 move, 4 expiry, 8 pickup, 16 regeneration, 32 delivery."""
+import os
+import sys
+import time
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rllib-warehouse_amd")]
+import torch  # noqa: E402
+import warehouse  # noqa: E402
+
+variant = sys.argv[1] if len(sys.argv) > 1 else "medium"
+na = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+B, C = 65536, 200
+env = warehouse.BatchedWarehouse(variant, B, na, seed=1)
+rew = torch.zeros((C, B, na), device="cuda")
+dn = torch.zeros((C, B), dtype=torch.uint8, device="cuda")
+masks = [0, 1, 2, 4, 8, 16, 32, 1 | 16, 63]
+res = {m: [] for m in masks}
+for rnd in range(5):
+    for m in masks:
+        os.environ["WH_ABLATE"] = str(m)
+        env.reset()
+        env.rollout(C, "greedy", 0.0, rewards=rew, dones=dn)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        env.rollout(C, "greedy", 0.0, rewards=rew, dones=dn)
+        torch.cuda.synchronize()
+        res[m].append((time.perf_counter() - t0) / C * 1e6)
+os.environ["WH_ABLATE"] = "0"
+for m in masks:
+    v = sorted(res[m])
+    print(f"ablate={m:2d} us/step median={v[len(v)//2]:.3f} min={v[0]:.3f}")

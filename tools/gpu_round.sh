@@ -13,12 +13,14 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; cat gpurun_out/status.txt; exit $rc; fi
   return 0
 }
+i=0
 for s in "$@"; do
+  i=$((i+1))
   case "$s" in
     smoke)  step smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) step pytest 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     bench)  step bench 600 python bench.py ;;
-    *)      step custom 900 bash -c "$s" ;;
+    *)      step custom$i 900 bash -c "$s" ;;
   esac
 done
 cat gpurun_out/status.txt

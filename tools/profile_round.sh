@@ -14,3 +14,6 @@ run() { local name=$1 limit=$2; shift 2
 run trace 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline "$@"
 run fetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetch -o run -- python3 bench.py --no-cpu-baseline --steps 300 --warmup 20 "$@"
 run write 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -o run -- python3 bench.py --no-cpu-baseline --steps 300 --warmup 20 "$@"
+if [ -n "$SQ" ]; then
+  run sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -T --output-format csv -d $OUT/sq -o run -- python3 bench.py --no-cpu-baseline --steps 300 --warmup 20 "$@"
+fi
