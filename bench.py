@@ -85,6 +85,80 @@ def load_traffic(tag):
         return None
 
 
+def measure(env, mode, policy, K, W, chunk, dev, world, dist):
+    """Time K steps of `mode`; returns (elapsed_s_max_over_ranks, kernel_ms, steps_per_launch)."""
+    import torch
+
+    B, NA = env.B, env.agent_slots
+    stream = torch.cuda.current_stream(dev)
+    if mode == "graph":
+        rew = torch.zeros((1, B, NA), device=dev)
+        dn = torch.zeros((1, B), dtype=torch.uint8, device=dev)
+
+        def one():
+            env.rollout(1, policy, 0.0, rewards=rew, dones=dn)
+
+        for _ in range(max(W, 3)):
+            one()
+        torch.cuda.synchronize(dev)
+        G = min(K, 200)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(G):
+                one()
+        torch.cuda.synchronize(dev)
+
+        def run_steps(k):
+            for _ in range(k // G):
+                graph.replay()
+            for _ in range(k % G):
+                one()
+
+        def timed_unit():
+            graph.replay()
+        per_unit_launches, spl = G, 1
+    else:
+        C = chunk
+        rew = torch.zeros((C, B, NA), device=dev)
+        dn = torch.zeros((C, B), dtype=torch.uint8, device=dev)
+
+        def run_steps(k):
+            while k > 0:
+                c = min(C, k)
+                env.rollout(c, policy, 0.0, rewards=rew[:c], dones=dn[:c])
+                k -= c
+        run_steps(max(W, 1))
+
+        def timed_unit():
+            env.rollout(C, policy, 0.0, rewards=rew, dones=dn)
+        per_unit_launches, spl = 1, C
+
+    # ---------------- timed region: barrier + sync on both sides, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(K)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---------------- kernel duration: HIP events on the launch stream around back-to-back
+    # launches (a graph replay of G one-step launches, or one fused launch), median of 7
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(7)]
+    for a, b in evs:
+        a.record(stream)
+        timed_unit()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kms = sorted(a.elapsed_time(b) / per_unit_launches for a, b in evs)
+    return elapsed, kms[len(kms) // 2], spl
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,10 +168,11 @@ def main():
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--policy", default="greedy", choices=["greedy", "random"])
-    ap.add_argument("--mode", default="graph", choices=["graph", "fused"],
-                    help="graph: hipGraph of one-step launches (state round-trips HBM every step); "
-                         "fused: --chunk steps per launch, state in registers")
+    ap.add_argument("--mode", default="fused", choices=["graph", "fused"],
+                    help="fused: --chunk steps per launch, state in registers (headline); "
+                         "graph: hipGraph of one-step launches, state round-trips HBM every step")
     ap.add_argument("--chunk", type=int, default=200)
+    ap.add_argument("--no-alt", action="store_true", help="skip the other launch mode")
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpus)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -120,88 +195,22 @@ def main():
     env = warehouse.BatchedWarehouse(args.variant, B, NA, seed=1234, env_offset=rank * B, device=dev)
     env.reset()
     words = env.layout.words_per_env
-    stream = torch.cuda.current_stream(dev)
+    out_b = 4 * NA + 1                       # rewards f32 x NA + done u8, per env-step
 
-    if args.mode == "graph":
-        rew = torch.zeros((1, B, NA), device=dev)
-        dn = torch.zeros((1, B), dtype=torch.uint8, device=dev)
-
-        def one():
-            env.rollout(1, args.policy, 0.0, rewards=rew, dones=dn)
-
-        for _ in range(max(W, 3)):
-            one()
-        torch.cuda.synchronize(dev)
-        G = min(K, 200)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(G):
-                one()
-        torch.cuda.synchronize(dev)
-
-        def run_steps(k):
-            for _ in range(k // G):
-                graph.replay()
-            for _ in range(k % G):
-                one()
-        per_launch_steps = 1
-    else:
-        C = args.chunk
-        rew = torch.zeros((C, B, NA), device=dev)
-        dn = torch.zeros((C, B), dtype=torch.uint8, device=dev)
-
-        def run_steps(k):
-            while k > 0:
-                c = min(C, k)
-                env.rollout(c, args.policy, 0.0, rewards=rew[:c], dones=dn[:c])
-                k -= c
-        run_steps(max(W, 1))
-        per_launch_steps = C
-
-    # ---------------- timed region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(K)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # ---------------- kernel duration for the roofline: HIP events on the launch stream around
-    # back-to-back launches (graph replays of G one-step launches, or single fused launches)
-    n_ev = 7
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-    c1 = per_launch_steps
-    if args.mode == "graph":
-        launches_per_ev = G
-        for a, b in evs:
-            a.record(stream)
-            graph.replay()
-            b.record(stream)
-    else:
-        launches_per_ev = 1
-        for a, b in evs:
-            a.record(stream)
-            env.rollout(c1, args.policy, 0.0, rewards=rew, dones=dn)
-            b.record(stream)
-    torch.cuda.synchronize(dev)
-    kms = sorted(a.elapsed_time(b) / launches_per_ev for a, b in evs)
-    kernel_ms = kms[n_ev // 2]   # median
-    if args.mode == "graph":
-        bytes_per_env_step = 2 * 4 * words + 4 * NA + 1
-        bytes_per_launch = B * bytes_per_env_step
-    else:
-        bytes_per_env_step = (2 * 4 * words + c1 * (4 * NA + 1)) / c1
-        bytes_per_launch = B * (2 * 4 * words + c1 * (4 * NA + 1))
+    elapsed, kernel_ms, spl = measure(env, args.mode, args.policy, K, W, args.chunk, dev, world, dist)
+    value = world * B * NA * K / elapsed
+    bytes_per_launch = B * (2 * 4 * words + spl * out_b)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    alt = None
+    if not args.no_alt:
+        other = "graph" if args.mode == "fused" else "fused"
+        el2, kms2, spl2 = measure(env, other, args.policy, K, W, args.chunk, dev, world, dist)
+        bpl2 = B * (2 * 4 * words + spl2 * out_b)
+        alt = {"mode": other, "value": world * B * NA * K / el2, "ms_per_step": el2 * 1e3 / K,
+               "kernel_ms": kms2, "steps_per_launch": spl2, "bytes_per_launch": bpl2,
+               "roofline_frac": bpl2 / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               "traffic": load_traffic(f"{args.variant}_n{NA}_{other}")}
 
-    total_agent_steps = world * B * NA * K
-    value = total_agent_steps / elapsed
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -220,7 +229,7 @@ def main():
                 "workload": f"C3: {args.variant} N={NA}, B={B} envs/GPU, {args.policy} policy fused with "
                             f"step + auto-reset (device-resident rollout)",
                 "envs_per_gpu": B, "agents": NA, "variant": args.variant, "policy": args.policy,
-                "launch": "hipGraph of 1-step launches" if args.mode == "graph" else f"{c1} steps per launch",
+                "launch": "hipGraph of 1-step launches" if args.mode == "graph" else f"{spl} steps per launch",
                 "parallelism": f"independent env shards x{world}, no collectives",
             },
             "roofline": {
@@ -230,11 +239,15 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": load_traffic(f"{args.variant}_n{NA}_{args.mode}"),
-                "kernel": "k_step<Cfg<16,9,3,8>, greedy>" if args.variant == "medium" and NA == 8 else "k_step",
+                "kernel": f"k_step<Cfg<D,R,racks,{NA}>, {args.policy}>",
                 "kernel_ms": kernel_ms,
+                "steps_per_launch": spl,
                 "bytes_per_launch": bytes_per_launch,
-                "bytes_per_env_step": bytes_per_env_step,
+                "bytes_per_env_step": bytes_per_launch / B / spl,
+                "note": "algorithmic bytes = 2 x packed state + per-step rewards/dones; the fused kernel "
+                        "keeps state in registers and is VALU-issue bound (DESIGN.md, Roofline)",
             },
+            "alt_launch_mode": alt,
         }
         if not args.no_cpu_baseline:
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)

@@ -410,7 +410,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
 // core.py:267-368 on one env held in registers.  Returns done.  No data-dependent branches:
 // LDS side effects are predicated through neutral operands (and ~0 / or 0 / the scratch word),
 // so each phase is one basic block and its LDS reads issue back to back.
-template <class C>
+template <class C, bool ORDERED>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
                                          const int32_t* __restrict__ actions_g,
@@ -436,7 +436,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         const uint32_t p = s.ag[i] & XY16;
         atomicOr(&L.occ[p >> 16][tid], (i < (int)n) ? (1u << (p & 31u)) : 0u);
       }
-      const bool ordered = order != nullptr;
+      constexpr bool ordered = ORDERED;   // action-dict order (drop-in single env only)
       if (ordered) {
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
@@ -671,7 +671,7 @@ struct StepParams {
   int32_t ablate;  // timing-only phase skips (env WH_ABLATE), never set in normal use
 };
 
-template <class C, int POLICY>
+template <class C, int POLICY, bool ORDERED>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
   load_tables<C>(L.tbl, a.tables);
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t d[C::NAM];
     if (POLICY == POL_EXTERNAL) {
-      const bool have = a.phase != PH_REGEN && a.order == nullptr;   // REGEN reads no actions
+      const bool have = a.phase != PH_REGEN && !ORDERED;   // REGEN reads no actions
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         uint32_t mv = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
       policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
+    const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
                                   (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, a.ablate);
     if (a.phase != PH_REGEN) {
       if (a.rewards) store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid);
@@ -1061,6 +1061,7 @@ int device_tables(const Geometry& g, int expect_words, const uint32_t** out) {
 struct Kernels {
   int D, R, NR, NAM;
   void (*step[3])(StepParams);
+  void (*step_ordered)(StepParams);
   void (*reset)(ResetParams);
   void (*observe)(const uint32_t*, int64_t, int, const uint32_t*, float*);
   int tblw, nv;
@@ -1071,9 +1072,10 @@ Kernels make_kernels() {
   using C = Cfg<D, R, NR, NAM>;
   Kernels k;
   k.D = D; k.R = R; k.NR = NR; k.NAM = NAM;
-  k.step[0] = k_step<C, POL_EXTERNAL>;
-  k.step[1] = k_step<C, POL_GREEDY>;
-  k.step[2] = k_step<C, POL_RANDOM>;
+  k.step[0] = k_step<C, POL_EXTERNAL, false>;
+  k.step[1] = k_step<C, POL_GREEDY, false>;
+  k.step[2] = k_step<C, POL_RANDOM, false>;
+  k.step_ordered = k_step<C, POL_EXTERNAL, true>;
   k.reset = k_reset<C>;
   k.observe = k_observe<C>;
   k.tblw = C::TBLW;
@@ -1210,7 +1212,8 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   a.tables = tab;
   const char* abl = getenv("WH_ABLATE");   // timing experiments only (tools/ablate.py)
   a.ablate = abl ? atoi(abl) : 0;
-  hipLaunchKernelGGL(k->step[policy], grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
+  void (*kern)(StepParams) = (a.order != nullptr && policy == POL_EXTERNAL) ? k->step_ordered : k->step[policy];
+  hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());
 }
 
