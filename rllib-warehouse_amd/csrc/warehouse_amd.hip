@@ -426,70 +426,9 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i) rew[i] = 0.0f;
 
-    // ---- move + collision, sequential in action-dict order (core.py:275-300)
-    asm volatile("; PHASE move" ::: "memory");
-    if (!(ablate & 2)) {
-#pragma unroll
-      for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
-#pragma unroll
-      for (int i = 0; i < C::NAM; ++i) {
-        const uint32_t p = s.ag[i] & XY16;
-        atomicOr(&L.occ[p >> 16][tid], (i < (int)n) ? (1u << (p & 31u)) : 0u);
-      }
-      constexpr bool ordered = ORDERED;   // action-dict order (drop-in single env only)
-      if (ordered) {
-#pragma unroll
-        for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
-      }
-      // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
-      uint32_t kk[3 * C::NAM];
-#pragma unroll
-      for (int sidx = 0; sidx < C::NAM; ++sidx) {
-        bool live;
-        uint32_t a, dd;
-        int who = sidx;
-        if (ordered) {
-          who = (sidx < na) ? order[e * na + sidx] : -1;
-          live = who >= 0 && who < (int)n && who < C::NAM;
-          who = live ? who : 0;
-          a = L.agl[who][tid];
-          const uint32_t mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
-          dd = L.mv(mv > 8u ? 4u : mv);
-        } else {
-          live = sidx < (int)n;
-          a = s.ag[sidx];
-          dd = dstep[sidx];
-        }
-        const uint32_t p = a & XY16;
-        const uint32_t c = step16<C::D>(p, dd);
-        const bool occupied = (L.occ[c >> 16][tid] >> (c & 31u)) & 1u;
-        const uint32_t key = p | (c << 8);
-        uint32_t f = 0xFFFFFFFFu;
-#pragma unroll
-        for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
-        const bool ok = live && !occupied && f != 0u;
-        atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
-        atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
-        const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u);   // (x, py)
-        const uint32_t c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);   // (px, y)
-        const uint32_t dx = c ^ p;
-        const bool diag = ok && (dx & 0xFFFFu) && (dx >> 16);
-        kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
-        kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
-        kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
-        const uint32_t moved = ok ? ((a & ~XY16) | c) : a;
-        if (ordered)
-          L.agl[who][tid] = moved;
-        else
-          s.ag[sidx] = moved;
-      }
-      if (ordered) {
-#pragma unroll
-        for (int i = 0; i < C::NAM; ++i) s.ag[i] = L.agl[i][tid];
-      }
-    }
-
-    // ---- request expiry (core.py:303-306), 4 pickup points per op
+    // ---- request expiry (core.py:303-306), 4 pickup points per op.  Run before the move: expiry
+    //      reads no positions and the move reads no requests, so the two commute, and the pickup
+    //      table is final before the move loop -- which lets its lookups be issued inside it.
     asm volatile("; PHASE expire" ::: "memory");
     if (!(ablate & 4)) {
       uint32_t any_exp = 0;
@@ -506,20 +445,116 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       }
       if (__any(any_exp != 0u)) s.am = active_mask(s);   // rare: only reset-time requests expire
     }
+#pragma unroll
+    for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
 
-    // ---- pickups: gather for every agent against the pre-pickup table, then clear
+    // ---- move + collision, sequential in action-dict order (core.py:275-300)
+    asm volatile("; PHASE move" ::: "memory");
+    uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329)
+    bool looked = false;
+    if (!(ablate & 2)) {
+#pragma unroll
+      for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) {
+        const uint32_t p = s.ag[i] & XY16;
+        atomicOr(&L.occ[p >> 16][tid], (i < (int)n) ? (1u << (p & 31u)) : 0u);
+      }
+      // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
+      uint32_t kk[3 * C::NAM];
+      if (ORDERED) {   // drop-in single env: agents in action-dict order, records in LDS
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
+#pragma unroll
+        for (int sidx = 0; sidx < C::NAM; ++sidx) {
+          int who = (sidx < na) ? order[e * na + sidx] : -1;
+          const bool live = who >= 0 && who < (int)n && who < C::NAM;
+          who = live ? who : 0;
+          const uint32_t a = L.agl[who][tid];
+          const uint32_t mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
+          const uint32_t p = a & XY16;
+          const uint32_t c = step16<C::D>(p, L.mv(mv > 8u ? 4u : mv));
+          const bool occupied = (L.occ[c >> 16][tid] >> (c & 31u)) & 1u;
+          const uint32_t key = p | (c << 8);
+          uint32_t f = 0xFFFFFFFFu;
+#pragma unroll
+          for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
+          const bool ok = live && !occupied && f != 0u;
+          atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
+          atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
+          const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u), c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);
+          const uint32_t dxy = c ^ p;
+          const bool diag = ok && (dxy & 0xFFFFu) && (dxy >> 16);
+          kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
+          kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
+          kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
+          L.agl[who][tid] = ok ? ((a & ~XY16) | c) : a;
+        }
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) s.ag[i] = L.agl[i][tid];
+      } else {
+        // Ascending agent order.  Every agent moves only on its own turn, so all candidate cells
+        // are known up front.  The occupancy word for agent s+1 is read one turn early (before
+        // agent s updates the grid) and corrected in registers for agent s's clear/set, so no
+        // LDS round trip sits on the serial chain; agent s's pickup lookups (cell -> point, point
+        // -> target byte, target -> cell) are issued on turns s, s+1, s+2.
+        uint32_t pp[C::NAM], cc[C::NAM];
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) {
+          pp[i] = s.ag[i] & XY16;
+          cc[i] = step16<C::D>(pp[i], dstep[i]);
+        }
+        uint32_t raw = L.occ[cc[0] >> 16][tid];
+        bool okp = false;
+#pragma unroll
+        for (int sidx = 0; sidx < C::NAM; ++sidx) {
+          const uint32_t p = pp[sidx], c = cc[sidx], a = s.ag[sidx];
+          bool occupied = (raw >> (c & 31u)) & 1u;
+          if (sidx > 0) {   // agent sidx-1 cleared its old cell, then set its new one
+            const bool set = okp && c == cc[sidx - 1];
+            const bool clr = okp && c == pp[sidx - 1];
+            occupied = set || (occupied && !clr);
+          }
+          if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
+          const uint32_t key = p | (c << 8);
+          uint32_t f = 0xFFFFFFFFu;
+#pragma unroll
+          for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
+          const bool ok = (sidx < (int)n) && !occupied && f != 0u;
+          atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
+          atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
+          const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u), c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);
+          const uint32_t dxy = c ^ p;
+          const bool diag = ok && (dxy & 0xFFFFu) && (dxy >> 16);
+          kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
+          kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
+          kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
+          const uint32_t moved = ok ? ((a & ~XY16) | c) : a;
+          s.ag[sidx] = moved;
+          okp = ok;
+          cp[sidx] = L.cell_pickup(moved & XY16);
+          if (sidx >= 1) tb[sidx - 1] = *L.ptl_byte(cp[sidx - 1] ? cp[sidx - 1] - 1u : 0u, tid);
+          if (sidx >= 2) dst[sidx - 2] = L.dst((tb[sidx - 2] - 1u) & 63u);
+        }
+        tb[C::NAM - 1] = *L.ptl_byte(cp[C::NAM - 1] ? cp[C::NAM - 1] - 1u : 0u, tid);
+        if (C::NAM >= 2) dst[C::NAM - 2] = L.dst((tb[C::NAM - 2] - 1u) & 63u);
+        dst[C::NAM - 1] = L.dst((tb[C::NAM - 1] - 1u) & 63u);
+        looked = true;
+      }
+    }
+
+    // ---- pickups: every agent decided against the pre-pickup table, then the table is cleared
     //      (core.py:309-335; two agents on one point both pick it up)
     asm volatile("; PHASE pickup" ::: "memory");
     if (!(ablate & 8)) {
+      if (!looked) {
 #pragma unroll
-      for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
-      uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];
+        for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
+        for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(cp[i] ? cp[i] - 1u : 0u, tid);
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(cp[i] ? cp[i] - 1u : 0u, tid);
-#pragma unroll
-      for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
+        for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
+      }
       uint64_t picked = 0;
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
@@ -683,6 +718,10 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
   load_env<C>(s, a.state, a.B, e, a.na);
+  // Drain the state loads here.  Their first uses are inside the step loop, so otherwise the
+  // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
+  // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
 
   if (a.phase == PH_POLICY) {
     uint32_t d[C::NAM];
@@ -756,469 +795,6 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
     reset_philox<C>(s, L, Keys{a.k0, a.k1}, (uint32_t)(a.env_offset + e), a.na, a.variable_n,
                     (uint32_t)a.W, tid);
   store_env<C>(s, a.state, a.B, e, a.na);
-}
-
-// ============================================================================= lane-pair kernels
-// One env on two lanes (2k, 2k+1) of a wave: B = 65,536 envs become 2,048 waves, two per SIMD, so
-// the SIMD can alternate between waves (a lone wave issues one VALU per 4 cycles) and one wave's
-// LDS round trips hide behind the other's work.  Lane h = lane & 1 owns agents i = 2m+h and
-// pickup words w = 2m+h; header, episode, the open-request mask and the request list are kept by
-// both lanes.  Exchanges are DPP quad_perm [1,0,3,2] moves (one VALU, no LDS).  The sequential
-// move loop (core.py:279-300) needs one exchange of the mover's (from | to << 8) key and one of
-// the partial forbidden-key minimum per agent; regeneration runs both selects of an item in one
-// select_bit64 (lane 0: the pickup, lane 1: its target, core.py:339-350).
-constexpr int EPB = BT / 2;   // envs per workgroup
-
-__device__ __forceinline__ uint32_t xch(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint64_t xch64(uint64_t v) {
-  return (uint64_t)xch((uint32_t)v) | ((uint64_t)xch((uint32_t)(v >> 32)) << 32);
-}
-
-template <class C>
-struct Regs2 {
-  static constexpr int NAH = (C::NAM + 1) / 2;
-  static constexpr int PWH = (C::PW + 1) / 2;
-  uint32_t hdr, epi;
-  uint32_t ag[NAH];     // agent 2m+h
-  uint32_t pt[PWH];     // pickup target word 2m+h
-  uint32_t pm[PWH];     // pickup timer word 2m+h
-  uint64_t am;          // open requests (full set, both lanes)
-};
-
-template <class C>
-struct Lds2 {
-  uint32_t tbl[C::TBLW];
-  uint32_t occ[C::D][EPB];           // per env: occupancy row y, bit x
-  uint32_t ptl[C::PW + 1][EPB];      // per env: pickup target bytes (+ scratch word)
-  float stg[EPB * C::NAM];           // per env reward rows, for coalesced stores
-  __device__ __forceinline__ uint32_t cell_pickup(uint32_t xy16) const {
-    return reinterpret_cast<const uint8_t*>(tbl)[(xy16 & 31u) | (xy16 >> 11)];
-  }
-  __device__ __forceinline__ uint32_t rp(uint32_t j) const { return tbl[C::T.rp / 4 + j]; }
-  __device__ __forceinline__ uint32_t tag(uint32_t j) const { return tbl[C::T.tag / 4 + j]; }
-  __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
-  __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
-  __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
-  __device__ __forceinline__ uint8_t* ptl_byte(uint32_t j, int pi) {
-    return reinterpret_cast<uint8_t*>(&ptl[j >> 2][pi]) + (j & 3u);
-  }
-};
-
-template <class C>
-__device__ __forceinline__ uint64_t partial_mask2(const Regs2<C>& s, int h) {
-  uint64_t am = 0;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::PWH; ++m)
-    am |= (uint64_t)nib_of(nz_hi(s.pt[m])) << (4 * (2 * m + h));   // word 2m+h -> bits 8m+4h..
-  return am;
-}
-
-template <class C>
-__device__ __forceinline__ void load_env2(Regs2<C>& s, const uint32_t* __restrict__ st, int64_t B,
-                                          int64_t e, int na, int h) {
-  const uint32_t hw = st[(int64_t)h * B + e];
-  const uint32_t ow = xch(hw);
-  s.hdr = h ? ow : hw;
-  s.epi = h ? hw : ow;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::NAH; ++m) {
-    const int i = 2 * m + h;
-    s.ag[m] = (i < na) ? st[(int64_t)(2 + i) * B + e] : IDLE;
-  }
-  const int wpt = 2 + na;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::PWH; ++m) {
-    const int w = 2 * m + h;
-    s.pt[m] = (w < C::PW) ? st[(int64_t)(wpt + w) * B + e] : 0u;
-    s.pm[m] = (w < C::PW) ? st[(int64_t)(wpt + C::PW + w) * B + e] : 0u;
-  }
-  const uint64_t mine = partial_mask2(s, h);
-  s.am = mine | xch64(mine);
-}
-
-template <class C>
-__device__ __forceinline__ void store_env2(const Regs2<C>& s, uint32_t* __restrict__ st, int64_t B,
-                                           int64_t e, int na, int h) {
-  st[(int64_t)h * B + e] = h ? s.epi : s.hdr;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::NAH; ++m) {
-    const int i = 2 * m + h;
-    if (i < na) st[(int64_t)(2 + i) * B + e] = s.ag[m];
-  }
-  const int wpt = 2 + na;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::PWH; ++m) {
-    const int w = 2 * m + h;
-    if (w < C::PW) {
-      st[(int64_t)(wpt + w) * B + e] = s.pt[m];
-      st[(int64_t)(wpt + C::PW + w) * B + e] = s.pm[m];
-    }
-  }
-}
-
-// core.py:167-221 with philox draws, same stream layout as reset_philox (both lanes walk the
-// request draws; lane 0 selects the pickup and lane 1 the target of each item in one select).
-template <class C>
-__device__ __forceinline__ void reset_philox2(Regs2<C>& s, Lds2<C>& L, const Keys& k, uint32_t gid,
-                                              int na, int variable_n, uint32_t W, int h, int pi) {
-  const uint32_t ep = s.epi + 1u;
-  Reader rd(k, gid, ep, 0u, PUR_RESET);
-  const uint32_t n = variable_n ? 1u + __umulhi(rd.word(0), (uint32_t)na) : (uint32_t)na;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::NAH; ++m) {
-    const int i = 2 * m + h;
-    const uint32_t w = rd.word(1 + (i < na ? i : 0));
-    const uint32_t cell = L.valid_cell(__umulhi(w, (uint32_t)C::NV));
-    s.ag[m] = (i < na && i < (int)n) ? (cell | IDLE) : IDLE;
-  }
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::PWH; ++m)
-    if (2 * m + h < C::PW) L.ptl[2 * m + h][pi] = 0u;
-  uint64_t remP = low_mask<C::P>(), remD = low_mask<C::DP>();
-  for (int j = 0; j < C::R; ++j) {
-    const uint32_t w1 = rd.word(1 + na + 2 * j), w2 = rd.word(2 + na + 2 * j);
-    const uint32_t r = h ? __umulhi(w2, (uint32_t)(C::DP - j)) : __umulhi(w1, (uint32_t)(C::P - j));
-    const int mine = select_bit64(h ? remD : remP, r);
-    const int other = (int)xch((uint32_t)mine);
-    const int sel = h ? other : mine, tg = h ? mine : other;
-    remP &= ~(1ull << sel);
-    remD &= ~(1ull << tg);
-    *L.ptl_byte((uint32_t)sel, pi) = (uint8_t)(tg + 1);
-  }
-  const uint64_t opened = low_mask<C::P>() & ~remP;
-  const uint32_t wb = W * 0x01010101u;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::PWH; ++m) {
-    const int w = 2 * m + h;
-    s.pt[m] = (w < C::PW) ? L.ptl[w][pi] : 0u;
-    s.pm[m] = (w < C::PW) ? (expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu) & wb) : 0u;
-  }
-  s.am = opened;
-  s.hdr = (n << 16) | (1u << 24);
-  s.epi = ep;
-}
-
-// solvers.py:27-58 for this lane's agents -> unit steps (packed i16)
-template <class C, int POLICY>
-__device__ __forceinline__ void policy_steps2(const Regs2<C>& s, const Lds2<C>& L, const Keys& k,
-                                              uint32_t gid, float p, int h,
-                                              uint32_t (&d)[Regs2<C>::NAH]) {
-  constexpr int NAH = Regs2<C>::NAH;
-  const uint32_t t = s.hdr & 0xFFFFu;
-  const uint32_t n = (s.hdr >> 16) & 0xFFu;
-  if (POLICY == POL_RANDOM) {
-#pragma unroll
-    for (int m = 0; m < NAH; ++m) {
-      const int i = 2 * m + h;   // word i of the RANDOM stream: block i >> 2, comp i & 3
-      const uint4 blk = stream_block(k, gid, s.epi, t, PUR_RANDOM, (uint32_t)(m >> 1));
-      const uint32_t w = h ? comp(blk, 2 * (m & 1) + 1) : comp(blk, 2 * (m & 1));
-      d[m] = L.mv(__umulhi(w, 9u));
-      (void)i;
-    }
-  } else {
-    const bool fresh = (s.hdr >> 24) & 1u;
-    uint32_t rp[C::R], tg[C::R];
-    uint64_t mm = s.am;
-#pragma unroll
-    for (int r = 0; r < C::R; ++r) {
-      const bool has = mm != 0ull;
-      const uint32_t j = has ? (uint32_t)__builtin_ctzll(mm) : 0u;
-      const uint32_t a = L.rp(j), b = L.tag(j);
-      rp[r] = has ? a : XY16;
-      tg[r] = has ? b : 0xFFFFu;
-      mm &= mm - 1ull;
-    }
-    constexpr uint32_t null16 = (uint32_t)(C::D / 2) | ((uint32_t)(C::D / 2) << 16);
-#pragma unroll
-    for (int m = 0; m < NAH; ++m) {
-      const uint32_t a = s.ag[m];
-      const uint32_t pos = a & XY16;
-      uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-      for (int r = 0; r < C::R; ++r) best = min(best, __builtin_amdgcn_sad_hi_u8(pos, rp[r], tg[r]));
-      const uint32_t near = ((best >> 5) & 31u) | ((best & 31u) << 16);
-      const uint32_t dst = (a >> 8) & XY16;
-      const bool carrying = (a & 0xFF00u) != 0xFF00u;
-      uint32_t goal = carrying ? dst : near;
-      goal = fresh ? null16 : goal;
-      d[m] = pk_min_i16(pk_max_i16(pk_sub_i16(goal, pos), 0xFFFFFFFFu), 0x00010001u);
-    }
-    if (p > 0.0f) {
-#pragma unroll
-      for (int m = 0; m < NAH; ++m) {   // agent i = 2m+h uses words 2i, 2i+1 = block m, comps 2h, 2h+1
-        const uint4 blk = stream_block(k, gid, s.epi, t, PUR_POLICY, (uint32_t)m);
-        const uint32_t wc = h ? blk.z : blk.x, wa = h ? blk.w : blk.y;
-        const float u = (float)(wc >> 8) * (1.0f / 16777216.0f);
-        const uint32_t rnd = L.mv(__umulhi(wa, 9u));
-        d[m] = (u < p) ? rnd : d[m];
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) d[m] = (2 * m + h < (int)n) ? d[m] : 0u;
-}
-
-template <class C>
-__device__ __forceinline__ bool step_env2(Regs2<C>& s, Lds2<C>& L, const uint32_t (&dstep)[Regs2<C>::NAH],
-                                          const int32_t* __restrict__ regen, const Keys& k,
-                                          uint32_t gid, int64_t e, uint32_t T, uint32_t W,
-                                          float (&rew)[Regs2<C>::NAH], int h, int pi) {
-  constexpr int NAH = Regs2<C>::NAH, PWH = Regs2<C>::PWH;
-  const uint32_t n = (s.hdr >> 16) & 0xFFu;
-  const uint32_t t = ((s.hdr & 0xFFFFu) + 1u) & 0xFFFFu;       // core.py:267
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) rew[m] = 0.0f;
-
-  // ---- move + collision (core.py:275-300): candidates in parallel, resolution in agent order
-  uint32_t key[NAH];
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) {
-    const uint32_t p = s.ag[m] & XY16;
-    key[m] = p | (step16<C::D>(p, dstep[m]) << 8);
-  }
-#pragma unroll
-  for (int r = 0; r < (C::D + 1) / 2; ++r)
-    if (2 * r + h < C::D) L.occ[2 * r + h][pi] = 0u;
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) {
-    const uint32_t p = s.ag[m] & XY16;
-    atomicOr(&L.occ[p >> 16][pi], (2 * m + h < (int)n) ? (1u << (p & 31u)) : 0u);
-  }
-  uint32_t kk[3 * NAH];
-#pragma unroll
-  for (int j = 0; j < 3 * NAH; ++j) kk[j] = 0xFFFFFFFFu;
-#pragma unroll
-  for (int sidx = 0; sidx < C::NAM; ++sidx) {
-    const int m = sidx >> 1, owner = sidx & 1;
-    const bool mine = h == owner;
-    const uint32_t kp = xch(key[m]);
-    const uint32_t K = mine ? key[m] : kp;                       // (from | to << 8) of agent sidx
-    const uint32_t p = K & XY16, c = (K >> 8) & XY16;
-    const bool occupied = (L.occ[c >> 16][pi] >> (c & 31u)) & 1u;
-    uint32_t f = 0xFFFFFFFFu;
-#pragma unroll
-    for (int j = 0; j < 3 * ((sidx + 1) / 2) && j < 3 * NAH; ++j) f = min(f, kk[j] ^ K);
-    f = min(f, xch(f));
-    const bool ok = (sidx < (int)n) && !occupied && f != 0u;
-    const bool apply = ok && mine;                               // one lane updates the grid
-    atomicAnd(&L.occ[p >> 16][pi], apply ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
-    atomicOr(&L.occ[c >> 16][pi], apply ? (1u << (c & 31u)) : 0u);
-    const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u);
-    const uint32_t c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);
-    const uint32_t dxy = c ^ p;
-    const bool diag = apply && (dxy & 0xFFFFu) && (dxy >> 16);
-    kk[3 * m] = apply ? (c | (p << 8)) : kk[3 * m];
-    kk[3 * m + 1] = diag ? (c1 | (c2 << 8)) : kk[3 * m + 1];
-    kk[3 * m + 2] = diag ? (c2 | (c1 << 8)) : kk[3 * m + 2];
-    s.ag[m] = apply ? ((s.ag[m] & ~XY16) | c) : s.ag[m];
-  }
-
-  // ---- expiry (core.py:303-306), own words
-  uint32_t any_exp = 0;
-#pragma unroll
-  for (int m = 0; m < PWH; ++m) {
-    const uint32_t live = nz_hi(s.pt[m]);
-    const uint32_t tm = s.pm[m] - (live >> 7);
-    const uint32_t zero = ~((((tm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tm)) & 0x80808080u;
-    const uint32_t ex = zero & live;
-    const uint32_t msk = (ex >> 7) * 0xFFu;
-    any_exp |= ex;
-    s.pt[m] &= ~msk;
-    s.pm[m] = tm & ~msk;
-  }
-  if (__any(any_exp != 0u)) {
-    const uint64_t part = partial_mask2(s, h);
-    s.am = part | xch64(part);
-  }
-
-  // ---- pickups (core.py:309-335): every agent against the pre-pickup table, then clear
-#pragma unroll
-  for (int m = 0; m < PWH; ++m)
-    if (2 * m + h < C::PW) L.ptl[2 * m + h][pi] = s.pt[m];
-  uint32_t cp[NAH], tb[NAH], dst[NAH];
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) cp[m] = L.cell_pickup(s.ag[m] & XY16);
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) tb[m] = *L.ptl_byte(cp[m] ? cp[m] - 1u : 0u, pi);
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) dst[m] = L.dst((tb[m] - 1u) & 63u);
-  uint64_t picked = 0;
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) {
-    const uint32_t a = s.ag[m];
-    const bool take = (2 * m + h < (int)n) & (cp[m] != 0u) & ((a & 0xFF00u) == 0xFF00u) & (tb[m] != 0u);
-    s.ag[m] = take ? ((a & XY16) | (dst[m] << 8)) : a;
-    picked |= take ? (1ull << ((cp[m] - 1u) & 63u)) : 0ull;
-    rew[m] = take ? 1.0f : 0.0f;
-  }
-  picked |= xch64(picked);
-#pragma unroll
-  for (int m = 0; m < PWH; ++m) {
-    const uint32_t msk = expand_nib((uint32_t)(picked >> (4 * (2 * m + h))) & 0xFu);
-    s.pt[m] &= ~msk;
-    s.pm[m] &= ~msk;
-  }
-  s.am &= ~picked;
-
-  // ---- regeneration (core.py:338-351)
-  {
-    const uint64_t inactive = ~s.am & low_mask<C::P>();
-    const uint32_t nin = (uint32_t)__popcll(inactive);
-    const int kreq = C::R - C::P + (int)nin;
-    uint64_t rem = inactive, used = 0, opened = 0;
-    uint32_t first_t = 0;
-    uint4 blk = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int j = 0; j < C::R; ++j) {
-      if (__any(j < kreq)) {
-        const bool act_j = j < kreq;
-        int sel, tgi;
-        if (regen) {
-          const uint32_t rpos = act_j ? (uint32_t)regen[e * 2 * C::R + j] : 0u;
-          tgi = act_j ? regen[e * 2 * C::R + C::R + j] : 0;
-          sel = (rpos < nin && (uint32_t)tgi < (uint32_t)C::DP) ? select_bit64(inactive, rpos) : C::P;
-        } else {
-          if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
-          const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
-          const uint32_t r1 = __umulhi(w1, nin - (uint32_t)j);
-          const uint32_t r2 = __umulhi(w2, (uint32_t)(C::DP - j));
-          int res;
-          if (j == 0)
-            res = h ? (int)r2 : select_bit64(rem, r1);
-          else if (j == 1)
-            res = h ? (int)(r2 + (r2 >= first_t ? 1u : 0u)) : select_bit64(rem, r1);
-          else
-            res = select_bit64(h ? (~used & low_mask<C::DP>()) : rem, h ? r2 : r1);
-          const int other = (int)xch((uint32_t)res);
-          sel = h ? other : res;
-          tgi = h ? res : other;
-          if (j == 0) first_t = r2;
-        }
-        const bool apply = act_j && sel < C::P;
-        rem &= apply ? ~(1ull << (sel & 63)) : ~0ull;
-        used |= apply ? (1ull << (tgi & 63)) : 0ull;
-        opened |= apply ? (1ull << (sel & 63)) : 0ull;
-        *L.ptl_byte(apply ? (uint32_t)sel : (uint32_t)(4 * C::PW), pi) = (uint8_t)(tgi + 1);
-      }
-    }
-    if (__any(opened != 0ull)) {
-      const uint32_t wb = W * 0x01010101u;
-#pragma unroll
-      for (int m = 0; m < PWH; ++m) {
-        const int w = 2 * m + h;
-        const uint32_t msk = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu);
-        const uint32_t lw = (w < C::PW) ? L.ptl[w][pi] : 0u;
-        s.pt[m] = (s.pt[m] & ~msk) | (lw & msk);
-        s.pm[m] = (s.pm[m] & ~msk) | (wb & msk);
-      }
-    }
-    s.am |= opened;
-  }
-
-  // ---- deliveries (core.py:354-368)
-#pragma unroll
-  for (int m = 0; m < NAH; ++m) {
-    const uint32_t a = s.ag[m];
-    const bool arrived = ((a >> 8) & XY16) == (a & XY16);
-    s.ag[m] = arrived ? (a | IDLE) : a;
-    rew[m] += arrived ? 1.0f : 0.0f;
-  }
-  s.hdr = t | (n << 16);
-  return t >= T;                                                 // core.py:438
-}
-
-// rewards[B, na] from lane pairs: rows go to LDS, each wave copies its 32 envs' contiguous
-// 32*na-float block back with lane-contiguous stores.
-template <class C>
-__device__ __forceinline__ void store_rewards2(Lds2<C>& L, const float (&rew)[Regs2<C>::NAH],
-                                               float* out, int64_t B, int64_t e, int na, int h, int tid) {
-  const int pi = tid >> 1;
-  const int64_t e0 = e - ((tid & 63) >> 1);          // first env of this wave
-  if (B - e0 < 32) {                                 // tail wave: direct rows
-#pragma unroll
-    for (int m = 0; m < Regs2<C>::NAH; ++m)
-      if (2 * m + h < na) out[e * na + 2 * m + h] = rew[m];
-    return;
-  }
-  float* stg = L.stg + (pi & ~31) * na;              // this wave's 32 rows
-  const int er = pi & 31;
-#pragma unroll
-  for (int m = 0; m < Regs2<C>::NAH; ++m)
-    if (2 * m + h < na) stg[er * na + 2 * m + h] = rew[m];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int lane = tid & 63;
-  float* wout = out + e0 * na;
-  if ((reinterpret_cast<uintptr_t>(wout) & 15u) == 0 && (na & 7) == 0) {
-#pragma unroll
-    for (int q = 0; q < (C::NAM + 7) / 8; ++q)       // 32*na floats = na/8 x (64 lanes x 16 B)
-      if (8 * q < na)
-        reinterpret_cast<float4*>(wout)[lane + 64 * q] = reinterpret_cast<const float4*>(stg)[lane + 64 * q];
-  } else {
-#pragma unroll
-    for (int q = 0; q < (C::NAM + 1) / 2; ++q)
-      if (lane + 64 * q < 32 * na) wout[lane + 64 * q] = stg[lane + 64 * q];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <class C, int POLICY>
-__global__ __launch_bounds__(BT) void k_step2(StepParams a) {
-  __shared__ Lds2<C> L;
-  load_tables<C>(L.tbl, a.tables);
-  __syncthreads();
-  const int tid = threadIdx.x, h = tid & 1, pi = tid >> 1;
-  const int64_t e = (int64_t)blockIdx.x * EPB + pi;
-  if (e >= a.B) return;                              // both lanes of a pair leave together
-  const Keys k{a.k0, a.k1};
-  const uint32_t gid = (uint32_t)(a.env_offset + e);
-  constexpr int NAH = Regs2<C>::NAH;
-  Regs2<C> s;
-  load_env2<C>(s, a.state, a.B, e, a.na, h);
-
-  if (a.phase == PH_POLICY) {
-    uint32_t d[NAH];
-    policy_steps2<C, POLICY>(s, L, k, gid, a.p, h, d);
-    const uint32_t n = (s.hdr >> 16) & 0xFFu;
-#pragma unroll
-    for (int m = 0; m < NAH; ++m) {
-      const int i = 2 * m + h;
-      if (i < a.na) a.actions_out[e * a.na + i] = (i < (int)n) ? (int32_t)action_of(d[m]) : 4;
-    }
-    return;
-  }
-  float ret = 0.0f;
-  for (int stp = 0; stp < a.steps; ++stp) {
-    uint32_t d[NAH];
-    if (POLICY == POL_EXTERNAL) {
-#pragma unroll
-      for (int m = 0; m < NAH; ++m) {
-        const int i = 2 * m + h;
-        const uint32_t mv = (i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
-        d[m] = L.mv(mv > 8u ? 4u : mv);
-      }
-    } else {
-      policy_steps2<C, POLICY>(s, L, k, gid, a.p, h, d);
-    }
-    float rew[NAH];
-    const bool done = step_env2<C>(s, L, d, a.regen, k, gid, e, (uint32_t)a.T, (uint32_t)a.W, rew, h, pi);
-    if (a.rewards) store_rewards2<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, h, tid);
-    if (a.dones && h == 0) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
-    if (a.returns) {
-#pragma unroll
-      for (int m = 0; m < NAH; ++m) ret += rew[m];
-    }
-    if (done && a.autoreset) reset_philox2<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, h, pi);
-  }
-  if (a.returns) {
-    ret += __shfl_xor(ret, 1);
-    if (h == 0) a.returns[e] += ret;
-  }
-  store_env2<C>(s, a.state, a.B, e, a.na, h);
 }
 
 // Observation rows: build a per-env byte image whose layout equals one row's value pool, then
@@ -1525,7 +1101,6 @@ struct Kernels {
   int D, R, NR, NAM;
   void (*step[3])(StepParams);
   void (*step_ordered)(StepParams);
-  void (*step2[3])(StepParams);
   void (*reset)(ResetParams);
   void (*observe)(const uint32_t*, int64_t, int, const uint32_t*, float*);
   int tblw, nv;
@@ -1540,9 +1115,6 @@ Kernels make_kernels() {
   k.step[1] = k_step<C, POL_GREEDY, false>;
   k.step[2] = k_step<C, POL_RANDOM, false>;
   k.step_ordered = k_step<C, POL_EXTERNAL, true>;
-  k.step2[0] = k_step2<C, POL_EXTERNAL>;
-  k.step2[1] = k_step2<C, POL_GREEDY>;
-  k.step2[2] = k_step2<C, POL_RANDOM>;
   k.reset = k_reset<C>;
   k.observe = k_observe<C>;
   k.tblw = C::TBLW;
@@ -1679,16 +1251,6 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   a.tables = tab;
   const char* abl = getenv("WH_ABLATE");   // timing experiments only (tools/ablate.py)
   a.ablate = abl ? atoi(abl) : 0;
-  // lane-pair kernels for whole steps and policy queries; one lane per env for action-dict order
-  // and the split phases of the drop-in single env (WH_LANES=1 forces one lane per env: A/B runs)
-  const char* lanes = getenv("WH_LANES");
-  const bool pair = (a.phase == PH_ALL || a.phase == PH_POLICY) && a.order == nullptr &&
-                    !(lanes && lanes[0] == '1');
-  if (pair) {
-    hipLaunchKernelGGL(k->step2[policy], dim3((unsigned)((B + EPB - 1) / EPB)), dim3(BT), 0,
-                       (hipStream_t)stream, a);
-    return hip_err(hipGetLastError());
-  }
   void (*kern)(StepParams) = (a.order != nullptr && policy == POL_EXTERNAL) ? k->step_ordered : k->step[policy];
   hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());

@@ -26,21 +26,6 @@ def wh():
     return warehouse
 
 
-@pytest.fixture(params=["pair", "lane"])
-def lanes(request):
-    """Run a test on both kernel families: lane pairs (default) and one lane per env."""
-    old = os.environ.get("WH_LANES")
-    if request.param == "lane":
-        os.environ["WH_LANES"] = "1"
-    else:
-        os.environ.pop("WH_LANES", None)
-    yield request.param
-    if old is None:
-        os.environ.pop("WH_LANES", None)
-    else:
-        os.environ["WH_LANES"] = old
-
-
 def canon(env):
     c = env.to_canonical()
     return {k: v.cpu().numpy() for k, v in c.items()}
@@ -54,7 +39,7 @@ def g1_runs(variant):
 
 @pytest.mark.parametrize("variant", ["small", "medium", "large"])
 @pytest.mark.parametrize("ordered", [True, False])
-def test_g1_episodes_injected(wh, lanes, variant, ordered):
+def test_g1_episodes_injected(wh, variant, ordered):
     """Whole 200-step reference episodes, all (variant, N, seed) runs batched as B envs."""
     runs = g1_runs(variant)
     if not ordered:
@@ -98,7 +83,7 @@ def test_g1_episodes_injected(wh, lanes, variant, ordered):
 
 
 @pytest.mark.parametrize("variant", ["small", "medium", "large"])
-def test_g2_dense_transitions(wh, lanes, variant):
+def test_g2_dense_transitions(wh, variant):
     g = np.load(os.path.join(GOLDEN, f"g2_{variant}.npz"))
     B = len(g["n"])
     env = wh.BatchedWarehouse(variant, B, train=True)
@@ -144,7 +129,7 @@ def assert_same(c, S, msg=""):
     np.testing.assert_array_equal(c["episode"].astype(np.uint32), S.episode, err_msg=msg)
 
 
-def test_c2_small_random_actions_philox(wh, lanes):
+def test_c2_small_random_actions_philox(wh):
     """Config 2: B=4096 Small envs x 4 agents, random actions, step kernel vs oracle, 210 steps
     (crosses the t=T boundary; no auto-reset in wh_step)."""
     B, seed = 4096, 99
@@ -169,7 +154,7 @@ def test_c2_small_random_actions_philox(wh, lanes):
 
 @pytest.mark.parametrize("variant,na,train,p", [("medium", 8, False, 0.0), ("large", 16, False, 0.0),
                                                 ("medium", 9, True, 0.3), ("small", 4, True, 0.1)])
-def test_policy_step_and_autoreset_vs_oracle(wh, lanes, variant, na, train, p):
+def test_policy_step_and_autoreset_vs_oracle(wh, variant, na, train, p):
     """wh_policy + wh_step + masked wh_reset, against the oracle with the philox contract."""
     B, seed = 2048, 7
     L = oc.layout_for(variant)
@@ -197,7 +182,7 @@ def test_policy_step_and_autoreset_vs_oracle(wh, lanes, variant, na, train, p):
 
 @pytest.mark.parametrize("variant,na,policy,p", [("medium", 8, "greedy", 0.0), ("large", 16, "greedy", 0.05),
                                                   ("small", 4, "random", 0.0)])
-def test_fused_rollout_equals_stepwise(wh, lanes, variant, na, policy, p):
+def test_fused_rollout_equals_stepwise(wh, variant, na, policy, p):
     """wh_rollout (K steps in one launch, auto-reset) == policy/step/reset launches == oracle."""
     import torch
 
@@ -225,7 +210,7 @@ def test_fused_rollout_equals_stepwise(wh, lanes, variant, na, policy, p):
     np.testing.assert_allclose(ret.cpu().numpy(), tot, rtol=0, atol=0)
 
 
-def test_c3_full_size_shard_invariance_and_spot_check(wh, lanes):
+def test_c3_full_size_shard_invariance_and_spot_check(wh):
     """Config 3 size (B=65536 Medium x 8, greedy, fused): 2 shards == 1 batch bit-exactly; a sampled
     subset of env ids equals the oracle; request/timer invariants hold for every env."""
     import torch
