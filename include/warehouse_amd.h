@@ -15,8 +15,9 @@
  *                               bit 24 fresh (set by reset: observation availabilities read 0,
  *                               core.py:233)
  *     w = 1            episode counter (bumped by every reset; keys the philox streams)
- *     w = 2 .. 2+NA-1  agent slot i: byte0 x, byte1 y, byte2 (delivery target + 1, 0 = idle)
- *                      (core.py:153-154)
+ *     w = 2 .. 2+NA-1  agent slot i: byte0 x, byte1 dx, byte2 y, byte3 dy (core.py:153-154), where
+ *                      (dx, dy) is the cell of the agent's delivery target and 0xFF,0xFF when it
+ *                      carries nothing; slots >= n hold 0xFF00FF00 (idle at (0,0))
  *     next P/4 words   pickup point j, byte j%4 of word j/4: (request target + 1, 0 = no request)
  *                      (core.py:158)
  *     next P/4 words   pickup point j: remaining wait (core.py:159; 0 when no request)
@@ -130,13 +131,42 @@ int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* ob
 int wh_policy(const wh_config* cfg, int64_t B, const uint32_t* state, int32_t policy, float p,
               int32_t* actions, uint64_t seed, int64_t env_offset, void* stream);
 
+/* Episode metrics of scripts/train.py:18-23 (on_episode_end: avg_agent_reward = episode return
+ * summed over agents / n, reported overall and per n), accumulated on the device.  Rewards are
+ * whole numbers, so returns are kept as integers and every total is exact and order-independent:
+ * the mean avg_agent_reward of the episodes with n agents is return_sum[n] / (n * episodes[n]).
+ * Bins are indexed by n (arrays of agent_slots + 1); the caller zeroes them (return_min to
+ * 0xFFFFFFFF).  `episode_return` is required when any bin pointer is set; others may be NULL.
+ * An episode is counted at the step whose done flag is set; continuing a done env without a reset
+ * counts it again (the reference has no guard after done either, core.py:438). */
+typedef struct wh_episode_stats {
+  uint32_t* episode_return;  /* [B]      running return of each env's current episode (read+write) */
+  uint64_t* return_sum;      /* [NA + 1] += return of every finished episode, binned by its n */
+  uint64_t* episodes;        /* [NA + 1] += finished episodes */
+  uint32_t* return_min;      /* [NA + 1] min= episode return */
+  uint32_t* return_max;      /* [NA + 1] max= episode return */
+} wh_episode_stats;
+
 /* Device-resident rollout: `steps` iterations of {policy, step, auto-reset at t >= T} in one
  * launch (the loop of baseline/run.py:42-62 without the host).  State stays in registers between
- * iterations.  rewards [steps,B,NA] / dones [steps,B] / returns [B] (+= sum of rewards) may each
- * be NULL.  Philox draws only. */
+ * iterations.  rewards [steps,B,NA] / dones [steps,B] / returns [B] (+= sum of rewards) / stats
+ * may each be NULL.  Philox draws only. */
 int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy,
-               float p, float* rewards, uint8_t* dones, float* returns, int32_t autoreset,
-               int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
+               float p, float* rewards, uint8_t* dones, float* returns, const wh_episode_stats* stats,
+               int32_t autoreset, int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
+
+/* One step of an RLlib-style vectorised sampler (the route scripts/train.py's workload takes:
+ * policy actions in, {obs, rewards, dones} out, done episodes restarted): wh_step with philox
+ * draws, then (autoreset != 0) a philox reset of every env whose episode ended -- Train variants
+ * (variable_n != 0) redraw n there, variants.py:69-71 -- then wh_observe into obs (NULL = skip).
+ * With autoreset the obs rows of a done env are the first rows of its next episode.
+ *   actions [B,NA] int32 0..8 (others act as 4 = stay); mask [B] uint8 or NULL: only envs with
+ *   mask != 0 are stepped (the others keep their state; their rewards/dones are not written);
+ *   rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats may be NULL. */
+int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
+                   const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
+                   const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
+                   uint64_t seed, int64_t env_offset, void* stream);
 
 /* Library build identification (e.g. "warehouse_amd gfx950 <date>"). */
 const char* wh_version(void);

@@ -653,10 +653,12 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 // of one strided row per lane.
 template <class C>
 __device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::NAM], float* out,
-                                              int64_t B, int64_t e, int na, int tid) {
+                                              int64_t B, int64_t e, int na, int tid, bool direct) {
   const int lane = tid & 63;
   const int64_t e0 = e - lane;
-  if (B - e0 < 64) {   // tail wave: lanes past B have exited, so no transpose -- one row per lane
+  // tail wave (lanes past B have exited) or masked step (unstepped lanes have exited): no
+  // transpose -- one row per lane
+  if (direct || B - e0 < 64) {
     float* row = out + e * na;
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i)
@@ -704,7 +706,40 @@ struct StepParams {
   int64_t env_offset;
   int32_t steps, phase, autoreset, variable_n;
   int32_t ablate;  // timing-only phase skips (env WH_ABLATE), never set in normal use
+  wh_episode_stats stats;   // all-NULL = off
+  const uint8_t* mask;      // [B] or NULL: envs to step (wh_vector_step)
 };
+
+// Folds the episodes this wave finished into the per-n bins of wh_episode_stats (the
+// on_episode_end metrics of scripts/train.py:18-23): one set of global atomics per distinct n in
+// the wave.  Sums, minima and maxima are built from ballots over bit slices, so only active lanes
+// contribute and the integer results do not depend on lane or wave order.
+__device__ __noinline__ void flush_episodes(bool fin, uint32_t n, uint32_t ret, const wh_episode_stats& st) {
+  uint64_t pend = __ballot(fin);
+  while (pend) {
+    const int leader = __ffsll((unsigned long long)pend) - 1;
+    const uint32_t nb = (uint32_t)__shfl((int)n, leader);
+    const bool g = fin && n == nb;
+    const uint64_t gm = __ballot(g);
+    pend &= ~gm;
+    uint64_t sum = 0;
+    uint32_t mn = 0, mx = 0;
+    bool cmin = g, cmax = g;
+    for (int b = 31; b >= 0; --b) {
+      const bool bit = (ret >> b) & 1u;
+      sum += (uint64_t)__popcll(__ballot(g && bit)) << b;
+      if (__ballot(cmax && bit)) { mx |= 1u << b; cmax = cmax && bit; }
+      if (__ballot(cmin && !bit)) cmin = cmin && !bit;
+      else mn |= 1u << b;
+    }
+    if ((int)__lane_id() == leader) {
+      if (st.return_sum) atomicAdd(&st.return_sum[nb], (unsigned long long)sum);
+      if (st.episodes) atomicAdd(&st.episodes[nb], (unsigned long long)__popcll(gm));
+      if (st.return_min) atomicMin(&st.return_min[nb], mn);
+      if (st.return_max) atomicMax(&st.return_max[nb], mx);
+    }
+  }
+}
 
 template <class C, int POLICY, bool ORDERED>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
@@ -714,6 +749,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const int tid = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
   if (e >= a.B) return;
+  if (a.mask && !a.mask[e]) return;
   const Keys k{a.k0, a.k1};
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
@@ -734,6 +770,8 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   }
 
   float ret = 0.0f;
+  const bool stats = a.stats.episode_return != nullptr;
+  uint32_t epr = stats ? a.stats.episode_return[e] : 0u;
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t d[C::NAM];
     if (POLICY == POL_EXTERNAL) {
@@ -753,16 +791,26 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
                                   (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, a.ablate);
     if (a.phase != PH_REGEN) {
-      if (a.rewards) store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid);
+      if (a.rewards) store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid,
+                                      a.mask != nullptr);
       if (a.dones) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
       if (a.returns) {
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) ret += rew[i];
       }
+      if (stats) {
+        float r = 0.0f;
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) r += rew[i];   // whole numbers: exact
+        epr += (uint32_t)r;
+        if (__any(done)) flush_episodes(done, (s.hdr >> 16) & 0xFFu, epr, a.stats);
+        if (done) epr = 0;
+      }
       if (done && a.autoreset) reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
     }
   }
   if (a.returns) a.returns[e] += ret;
+  if (stats) a.stats.episode_return[e] = epr;
   store_env<C>(s, a.state, a.B, e, a.na);
 }
 
@@ -797,56 +845,106 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
   store_env<C>(s, a.state, a.B, e, a.na);
 }
 
-// Observation rows: build a per-env byte image whose layout equals one row's value pool, then
-// every output float is img[desc(f) + row-adjust(i)] -- no per-feature branching.
-//   image bytes: [0] n, [1..R] availability, then R x (x,y) delivery targets, R x (x,y)
-//   positions, R x (px,py,dx,dy) requests.
-constexpr int OBS_EB = 64;  // envs per workgroup
+// Observation rows (core.py:371-432, reset rows core.py:224-260), HBM-write bound.
+// Each env's values live in a small byte image whose layout is one row's value pool:
+//   [0] n, [1..R] availability, R x (x,y) delivery targets, R x (x,y) positions,
+//   R x (px,py,dx,dy) requests (active slots, ascending pickup index).
+// Output float k of an env (k = i*L + f for agent row i, feature f) is img[src[fresh][k]] when
+// i < n, else 0.  src is a compile-time byte table per (R, NAM): every row's "other agents"
+// gather (skip row i; other_delivery_targets skips row 1 unless the episode is fresh, core.py:428
+// vs :256) is folded into it, so the write loop is branch-free.  A workgroup images 16 envs with
+// 16 lanes per env, then writes the group's contiguous [16 env x na x L] float region as float4s.
+// Small workgroups keep many groups in flight per CU, so one group's image build overlaps the
+// others' streaming stores.
+constexpr int OBS_EB = 16;        // envs per workgroup
+constexpr int OBS_PARTS = BT / OBS_EB;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Image offset of output value f of agent row i (sorted-key order, see wh_observe).
+template <int R>
+__host__ __device__ constexpr uint32_t obs_src(int i, int f, bool fresh) {
+  constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
+  if (f == 0) return 0;                                                    // num_agents
+  if (f < R) {                                                             // other_availabilities
+    const int j = f - 1;
+    return A0 + (j < i ? j : j + 1);
+  }
+  if (f < 3 * R - 2) {                                                     // other_delivery_targets
+    const int k = f - R, j = k >> 1, drop = fresh ? i : 1;
+    return G0 + 2 * (j < drop ? j : j + 1) + (k & 1);
+  }
+  if (f < 5 * R - 4) {                                                     // other_positions
+    const int k = f - (3 * R - 2), j = k >> 1;
+    return P0 + 2 * (j < i ? j : j + 1) + (k & 1);
+  }
+  if (f < 9 * R - 4) return Q0 + (f - (5 * R - 4));                        // requests
+  if (f == 9 * R - 4) return A0 + i;                                       // self_availability
+  if (f < 9 * R - 1) return G0 + 2 * i + (f - (9 * R - 3));                // self_delivery_target
+  return P0 + 2 * i + (f - (9 * R - 1));                                   // self_position
+}
+
+template <int R, int NAM>
+struct ObsSrc {
+  static constexpr int L = 9 * R + 1, W = (NAM * L + 3) / 4;
+  uint32_t w[2][W];
+};
+template <int R, int NAM>
+constexpr ObsSrc<R, NAM> make_obs_src() {
+  ObsSrc<R, NAM> t{};
+  constexpr int L = 9 * R + 1;
+  for (int fr = 0; fr < 2; ++fr)
+    for (int k = 0; k < NAM * L; ++k)
+      t.w[fr][k >> 2] |= obs_src<R>(k / L, k % L, fr != 0) << (8 * (k & 3));
+  return t;
+}
+template <int R, int NAM>
+__constant__ ObsSrc<R, NAM> kObsSrc = make_obs_src<R, NAM>();
 
 template <class C>
 struct ObsLds {
   static constexpr int IMG = (C::L + 3) & ~3;
+  static constexpr int SRCW = ObsSrc<C::R, C::NAM>::W;
   uint8_t img[OBS_EB][IMG];
-  uint8_t fresh[OBS_EB];
-  uint32_t desc[C::L];
-  uint32_t tbl[C::TBLW];
+  uint32_t lim[OBS_EB];          // n * L (floats of live rows) | fresh << 31
+  uint32_t ptw[OBS_EB][C::PW];   // pickup target words (nonzero byte = active slot)
+  uint32_t src[2][SRCW];
+  uint32_t rp[C::P];             // pickup cell, x | y << 16
+  uint32_t dst[C::DP];           // delivery cell, x | y << 16
 };
 
 template <class C>
 __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ state, int64_t B, int na,
                                                 const uint32_t* __restrict__ tables,
-                                                float* __restrict__ obs) {
+                                                float* __restrict__ obs, int quads) {
   __shared__ ObsLds<C> O;
-  constexpr int R = C::R, D = C::D;
+  constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C>::SRCW;
   constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
   const int tid = threadIdx.x;
-  load_tables<C>(O.tbl, tables);
-  // feature descriptors: base | stride << 10 | mode << 14 | j << 16
-  //   mode 0: fixed byte; 1: other row skip i; 2: other row skip (fresh ? i : 1); 3: own row
-  for (int f = tid; f < C::L; f += BT) {
-    uint32_t base, stride = 0, mode = 0, j = 0;
-    if (f == 0) { base = 0; }
-    else if (f < R) { j = f - 1; base = A0; stride = 1; mode = 1; }
-    else if (f < 3 * R - 2) { j = (f - R) >> 1; base = G0 + ((f - R) & 1); stride = 2; mode = 2; }
-    else if (f < 5 * R - 4) { j = (f - (3 * R - 2)) >> 1; base = P0 + ((f - (3 * R - 2)) & 1); stride = 2; mode = 1; }
-    else if (f < 9 * R - 4) { base = Q0 + (f - (5 * R - 4)); }
-    else if (f == 9 * R - 4) { base = A0; stride = 1; mode = 3; }
-    else if (f < 9 * R - 1) { base = G0 + (f - (9 * R - 3)); stride = 2; mode = 3; }
-    else { base = P0 + (f - (9 * R - 1)); stride = 2; mode = 3; }
-    O.desc[f] = base | (stride << 10) | (mode << 14) | (j << 16);
-  }
-  __syncthreads();
+  const uint32_t* srcg = &kObsSrc<C::R, C::NAM>.w[0][0];
+  for (int k = tid; k < 2 * SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
+  for (int k = tid; k < C::P; k += BT) O.rp[k] = tables[C::T.rp / 4 + k];
+  for (int k = tid; k < C::DP; k += BT) O.dst[k] = tables[C::T.dst / 4 + k];
+
   const int64_t e0 = (int64_t)blockIdx.x * OBS_EB;
-  if (tid < OBS_EB && e0 + tid < B) {
-    const int64_t e = e0 + tid;
+  const uint32_t nenv = (uint32_t)((B - e0) < OBS_EB ? (B - e0) : OBS_EB);
+  const int el = tid / OBS_PARTS, part = tid % OBS_PARTS;
+  const bool mine = (uint32_t)el < nenv;
+  const int64_t e = e0 + el;
+  const uint8_t nul = (uint8_t)(D / 2);
+  uint32_t n = 0;
+  bool fresh = false;
+  if (mine) {
     const uint32_t hdr = state[e];
-    const uint32_t n = (hdr >> 16) & 0xFFu;
-    const bool fresh = (hdr >> 24) & 1u;
-    uint8_t* im = O.img[tid];
-    const uint8_t nul = (uint8_t)(D / 2);
-    im[0] = (uint8_t)n;
-    for (int r = 0; r < R; ++r) {
-      const bool live = r < (int)n && r < na;
+    n = (hdr >> 16) & 0xFFu;
+    n = n < (uint32_t)na ? n : (uint32_t)na;
+    fresh = (hdr >> 24) & 1u;
+    uint8_t* im = O.img[el];
+    if (part == 0) {
+      im[0] = (uint8_t)n;
+      O.lim[el] = n * L | (fresh ? 0x80000000u : 0u);
+    }
+    for (int r = part; r < R; r += OBS_PARTS) {          // agent rows
+      const bool live = r < (int)n;
       const uint32_t a = live ? state[(2 + r) * B + e] : IDLE;
       const bool carry = (a & 0xFF00u) != 0xFF00u;
       im[A0 + r] = (uint8_t)((live && !fresh && !carry) ? 1 : 0);
@@ -856,15 +954,20 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
       im[P0 + 2 * r] = live ? (uint8_t)(a & 0xFFu) : nul;
       im[P0 + 2 * r + 1] = live ? (uint8_t)((a >> 16) & 0xFFu) : nul;
     }
-    const int wpt = 2 + na;
-    int r = 0;
-    for (int w = 0; w < C::PW; ++w) {
-      const uint32_t pt = state[(wpt + w) * B + e];
+    for (int w = part; w < C::PW; w += OBS_PARTS) O.ptw[el][w] = state[(2 + na + w) * B + e];
+  }
+  __syncthreads();
+  if (mine) {                                             // requests: ascending pickup index
+    uint8_t* im = O.img[el];
+    for (int w = part; w < C::PW; w += OBS_PARTS) {
+      uint32_t r = 0;
+      for (int v = 0; v < w; ++v) r += __popc(nz_hi(O.ptw[el][v]));
+      const uint32_t pt = O.ptw[el][w];
       for (int b = 0; b < 4; ++b) {
         const uint32_t tg = (pt >> (8 * b)) & 0xFFu;
-        if (tg && r < R) {
-          const uint32_t pxy = O.tbl[C::T.rp / 4 + 4 * w + b];
-          const uint32_t dxy = O.tbl[C::T.dst / 4 + ((tg - 1u) & 63u)];
+        if (tg && r < (uint32_t)R) {
+          const uint32_t pxy = O.rp[4 * w + b];
+          const uint32_t dxy = O.dst[(tg - 1u) % C::DP];
           im[Q0 + 4 * r] = (uint8_t)(pxy & 0xFFu);
           im[Q0 + 4 * r + 1] = (uint8_t)(pxy >> 16);
           im[Q0 + 4 * r + 2] = (uint8_t)(dxy & 0xFFu);
@@ -872,27 +975,43 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
           ++r;
         }
       }
+      if (w == C::PW - 1)      // fewer than R active slots never occurs after reset/step; keep rows defined
+        for (; r < (uint32_t)R; ++r)
+          im[Q0 + 4 * r] = im[Q0 + 4 * r + 1] = im[Q0 + 4 * r + 2] = im[Q0 + 4 * r + 3] = 0;
     }
-    O.fresh[tid] = fresh ? 1 : 0;
   }
   __syncthreads();
-  const int64_t nenv = (B - e0) < OBS_EB ? (B - e0) : OBS_EB;
-  const int64_t total = nenv * na * C::L;   // floats this block writes
-  float* out = obs + e0 * na * C::L;
-  for (int64_t o = tid; o < total; o += BT) {
-    const int el = (int)(o / (na * C::L));
-    const int rem = (int)(o - (int64_t)el * na * C::L);
-    const int i = rem / C::L;
-    const int f = rem - i * C::L;
-    const uint32_t d = O.desc[f];
-    const uint32_t base = d & 0x3FFu, stride = (d >> 10) & 0xFu, mode = (d >> 14) & 3u, j = d >> 16;
-    uint32_t row = 0;
-    if (mode == 1) row = (j < (uint32_t)i) ? j : j + 1;
-    else if (mode == 2) { const uint32_t drop = O.fresh[el] ? (uint32_t)i : 1u; row = (j < drop) ? j : j + 1; }
-    else if (mode == 3) row = (uint32_t)i;
-    const uint8_t* im = O.img[el];
-    const float v = (i < (int)im[0]) ? (float)im[base + stride * row] : 0.0f;
-    out[o] = v;
+  const uint32_t per_env = (uint32_t)na * L;
+  float* out = obs + e0 * per_env;
+  if (quads) {
+    // per_env % 4 == 0 and obs 16-byte aligned (checked on the host)
+    const uint32_t qe = per_env >> 2, total = nenv * qe;
+    const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
+    f32x4* out4 = reinterpret_cast<f32x4*>(out);
+    for (uint32_t q = tid; q < total; q += BT) {
+      const uint32_t el4 = __umulhi(q, magic);
+      const uint32_t k4 = q - el4 * qe;
+      const uint32_t lim = O.lim[el4];
+      const uint32_t sw = O.src[lim >> 31][k4];
+      const int live = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
+      const uint8_t* im = O.img[el4];
+      f32x4 v;
+      v.x = live > 0 ? (float)im[sw & 0xFFu] : 0.0f;
+      v.y = live > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
+      v.z = live > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
+      v.w = live > 3 ? (float)im[sw >> 24] : 0.0f;
+      out4[q] = v;
+    }
+  } else {
+    const uint32_t total = nenv * per_env;
+    const uint32_t magic = 0xFFFFFFFFu / per_env + 1u;
+    for (uint32_t o = tid; o < total; o += BT) {
+      const uint32_t el1 = __umulhi(o, magic);
+      const uint32_t k = o - el1 * per_env;
+      const uint32_t lim = O.lim[el1];
+      const uint8_t* sb = reinterpret_cast<const uint8_t*>(O.src[lim >> 31]);
+      out[o] = k < (lim & 0x7FFFFFFFu) ? (float)O.img[el1][sb[k]] : 0.0f;
+    }
   }
 }
 
@@ -1102,7 +1221,7 @@ struct Kernels {
   void (*step[3])(StepParams);
   void (*step_ordered)(StepParams);
   void (*reset)(ResetParams);
-  void (*observe)(const uint32_t*, int64_t, int, const uint32_t*, float*);
+  void (*observe)(const uint32_t*, int64_t, int, const uint32_t*, float*, int);
   int tblw, nv;
 };
 
@@ -1291,12 +1410,17 @@ int wh_policy(const wh_config* cfg, int64_t B, const uint32_t* state, int32_t po
   return launch_step(cfg, B, const_cast<uint32_t*>(state), policy, a, stream);
 }
 
+static bool stats_ok(const wh_episode_stats* st) {
+  return !st || st->episode_return || (!st->return_sum && !st->episodes && !st->return_min && !st->return_max);
+}
+
 int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy,
-               float p, float* rewards, uint8_t* dones, float* returns, int32_t autoreset,
-               int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream) {
+               float p, float* rewards, uint8_t* dones, float* returns, const wh_episode_stats* stats,
+               int32_t autoreset, int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream) {
   if ((policy != WH_POLICY_GREEDY && policy != WH_POLICY_RANDOM) || steps < 0) return WH_EINVAL;
-  if (!(p >= 0.0f && p <= 1.0f)) return WH_EINVAL;
+  if (!(p >= 0.0f && p <= 1.0f) || !stats_ok(stats)) return WH_EINVAL;
   StepParams a{};
+  if (stats) a.stats = *stats;
   a.rewards = rewards;
   a.dones = dones;
   a.returns = returns;
@@ -1319,9 +1443,34 @@ int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* ob
   if (rc) return rc;
   if (B == 0) return WH_OK;
   if (!state || !obs) return WH_EINVAL;
+  const int quads = ((g.NA * (9 * g.R + 1)) % 4 == 0) && ((uintptr_t)obs % 16 == 0);
   hipLaunchKernelGGL(k->observe, dim3((unsigned)((B + OBS_EB - 1) / OBS_EB)), dim3(BT), 0,
-                     (hipStream_t)stream, state, B, g.NA, tab, obs);
+                     (hipStream_t)stream, state, B, g.NA, tab, obs, quads);
   return hip_err(hipGetLastError());
+}
+
+int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
+                   const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
+                   const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
+                   uint64_t seed, int64_t env_offset, void* stream) {
+  if (B > 0 && !actions) return WH_EINVAL;
+  if (!stats_ok(stats)) return WH_EINVAL;
+  StepParams a{};
+  a.actions = actions;
+  a.mask = mask;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = 1;
+  a.phase = PH_ALL;
+  a.autoreset = autoreset ? 1 : 0;
+  a.variable_n = variable_n ? 1 : 0;
+  if (stats) a.stats = *stats;
+  int rc = launch_step(cfg, B, state, POL_EXTERNAL, a, stream);
+  if (rc || !obs) return rc;
+  return wh_observe(cfg, B, state, obs, stream);
 }
 
 }  // extern "C"

@@ -29,7 +29,7 @@ WH_POLICY_RANDOM = 2
 
 # every symbol include/warehouse_amd.h declares
 SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observe", "wh_policy",
-           "wh_rollout", "wh_version")
+           "wh_rollout", "wh_vector_step", "wh_version")
 
 
 class WhConfig(ctypes.Structure):
@@ -63,6 +63,16 @@ class WhResetDraws(ctypes.Structure):
     ]
 
 
+class WhEpisodeStats(ctypes.Structure):
+    _fields_ = [
+        ("episode_return", ctypes.c_void_p),
+        ("return_sum", ctypes.c_void_p),
+        ("episodes", ctypes.c_void_p),
+        ("return_min", ctypes.c_void_p),
+        ("return_max", ctypes.c_void_p),
+    ]
+
+
 class WarehouseNativeError(RuntimeError):
     pass
 
@@ -93,7 +103,9 @@ def lib() -> ctypes.CDLL:
     L.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P]
     L.wh_observe.argtypes = [_CFG, _I64, _P, _P, _P]
     L.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
-    L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _I32, _I32, _U64, _I64, _P]
+    _ST = ctypes.POINTER(WhEpisodeStats)
+    L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    L.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     for name in SYMBOLS:
         if name != "wh_version":
             getattr(L, name).restype = ctypes.c_int

@@ -8,6 +8,8 @@ STATE") as one int32 device tensor `state[words, B]` and drives the HIP kernels 
     observe()  -> wh_observe  per-agent observation rows     warehouse/core.py:224-260, 371-432
     policy()   -> wh_policy   greedy / random actions        baseline/solvers.py:27-58
     rollout()  -> wh_rollout  device-resident rollout loop   baseline/run.py:42-62
+    vector_step() -> wh_vector_step  sampler step: step + auto-reset + observation rows
+    EpisodeStats     on_episode_end metrics kept on the device  scripts/train.py:18-23
 
 Global env ids are `env_offset + e`; with philox draws a shard of env ids reproduces exactly the
 trajectories those ids have in any other sharding (multi-GPU is a straight per-device shard).
@@ -48,6 +50,64 @@ def _dev_i32(x, device, shape=None):
     return t
 
 
+class EpisodeStats:
+    """Device-side episode metrics of scripts/train.py:18-23 (`on_episode_end`): for every
+    finished episode avg_agent_reward = (episode return summed over agents) / n, reported over all
+    episodes ("avg_agent_reward_all") and per agent count n ("avg_agent_reward_{n}").  The kernels
+    bin integer returns by n (wh_episode_stats), so every figure here is exact."""
+
+    def __init__(self, num_envs: int, agent_slots: int, device):
+        z = dict(device=device)
+        self.agent_slots = int(agent_slots)
+        self.episode_return = torch.zeros(num_envs, dtype=torch.int32, **z)
+        self.return_sum = torch.zeros(agent_slots + 1, dtype=torch.int64, **z)
+        self.episodes = torch.zeros(agent_slots + 1, dtype=torch.int64, **z)
+        self.return_min = torch.full((agent_slots + 1,), -1, dtype=torch.int32, **z)   # 0xFFFFFFFF
+        self.return_max = torch.zeros(agent_slots + 1, dtype=torch.int32, **z)
+        self._c = nat.WhEpisodeStats(self.episode_return.data_ptr(), self.return_sum.data_ptr(),
+                                     self.episodes.data_ptr(), self.return_min.data_ptr(),
+                                     self.return_max.data_ptr())
+
+    @property
+    def ref(self):
+        return ctypes.byref(self._c)
+
+    def clear(self) -> None:
+        """Forget finished episodes (running episode returns are kept)."""
+        self.return_sum.zero_()
+        self.episodes.zero_()
+        self.return_min.fill_(-1)
+        self.return_max.zero_()
+
+    def bins(self) -> Dict[str, np.ndarray]:
+        return dict(return_sum=self.return_sum.cpu().numpy(), episodes=self.episodes.cpu().numpy(),
+                    return_min=self.return_min.cpu().numpy().view(np.uint32),
+                    return_max=self.return_max.cpu().numpy().view(np.uint32))
+
+    def custom_metrics(self) -> Dict[str, Dict[str, float]]:
+        return custom_metrics_from_bins(**self.bins())
+
+
+def custom_metrics_from_bins(return_sum, episodes, return_min, return_max) -> Dict[str, Dict[str, float]]:
+    """RLlib's custom_metrics summary (mean / min / max / count over episodes) of the
+    avg_agent_reward values on_episode_end records (scripts/train.py:18-23), from n-binned totals."""
+    out: Dict[str, Dict[str, float]] = {}
+    tot_avg, tot_cnt, lo, hi = 0.0, 0, np.inf, -np.inf
+    for n in range(1, len(episodes)):
+        c = int(episodes[n])
+        if c == 0:
+            continue
+        mean = int(return_sum[n]) / (n * c)
+        mn, mx = int(return_min[n]) / n, int(return_max[n]) / n
+        out[f"avg_agent_reward_{n}"] = dict(mean=mean, min=mn, max=mx, count=c)
+        tot_avg += int(return_sum[n]) / n
+        tot_cnt += c
+        lo, hi = min(lo, mn), max(hi, mx)
+    if tot_cnt:
+        out["avg_agent_reward_all"] = dict(mean=tot_avg / tot_cnt, min=lo, max=hi, count=tot_cnt)
+    return out
+
+
 class BatchedWarehouse:
     """`num_envs` episodes of one variant.  `train=True` gives the Train variants' per-episode
     agent count n ~ U{1..max_num_agents} (warehouse/variants.py:65-98) with max_num_agents slots."""
@@ -78,6 +138,13 @@ class BatchedWarehouse:
         self.n_inactive = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._obs = None
         self._cfgp = ctypes.byref(self.cfg)
+        self.stats: Optional[EpisodeStats] = None
+
+    def enable_episode_stats(self) -> EpisodeStats:
+        """Track on_episode_end metrics in rollout() / vector_step() from now on."""
+        if self.stats is None:
+            self.stats = EpisodeStats(self.B, self.agent_slots, self.device)
+        return self.stats
 
     # ------------------------------------------------------------------ plumbing
     @property
@@ -106,6 +173,11 @@ class BatchedWarehouse:
                                                None if nn is None else nn.data_ptr()))
         self._call("wh_reset", self.state.data_ptr(), nat.ptr(m), dp, int(self.train),
                    self.seed, self.env_offset, self.stream)
+        if self.stats is not None:   # a reset starts a new episode return
+            if m is None:
+                self.stats.episode_return.zero_()
+            else:
+                self.stats.episode_return.masked_fill_(m.bool(), 0)
         del keep
 
     def step(self, actions, order=None, regen=None, phase: int = nat.WH_PHASE_ALL
@@ -129,6 +201,26 @@ class BatchedWarehouse:
         self._call("wh_observe", self.state.data_ptr(), self._obs.data_ptr(), self.stream)
         return self._obs
 
+    def vector_step(self, actions, autoreset: bool = True, observe: bool = True, mask=None
+                    ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
+        """Sampler step (wh_vector_step): step every env (or those in the [B] bool `mask`) with
+        `actions` [B,NA] (philox draws), restart the envs whose episode ended (autoreset; Train
+        variants redraw n), then write the observation rows.  Returns env-owned (obs [B,NA,9R+1]
+        or None, rewards [B,NA], dones [B]); with autoreset the obs rows of a done env already
+        belong to its next episode.  Rewards/dones of envs outside `mask` are stale."""
+        a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        if observe and self._obs is None:
+            self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
+                                    device=self.device)
+        obs = self._obs if observe else None
+        self._call("wh_vector_step", self.state.data_ptr(), a.data_ptr(), nat.ptr(m), self.rewards.data_ptr(),
+                   self.dones.data_ptr(), nat.ptr(obs), None if self.stats is None else self.stats.ref,
+                   int(bool(autoreset)), int(self.train), self.seed, self.env_offset, self.stream)
+        return obs, self.rewards, self.dones
+
     def policy(self, kind: str = "greedy", p: float = 0.0) -> torch.Tensor:
         self._call("wh_policy", self.state.data_ptr(), POLICIES[kind], float(p), self.actions.data_ptr(),
                    self.seed, self.env_offset, self.stream)
@@ -143,7 +235,8 @@ class BatchedWarehouse:
             if t is not None and tuple(t.shape) != shape:
                 raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
         self._call("wh_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
-                   nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns), int(bool(autoreset)),
+                   nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
+                   None if self.stats is None else self.stats.ref, int(bool(autoreset)),
                    int(self.train), self.seed, self.env_offset, self.stream)
 
     # ------------------------------------------------------------------ canonical state

@@ -1,0 +1,182 @@
+"""RLlib-facing batched adapters over `BatchedWarehouse` (the route scripts/train.py's workload
+takes, scripts/train.py:29-43): many warehouse episodes on one MI355X presented to a sampler.
+
+* `WarehouseVectorEnv` -- the tensor fast path, shaped like ray.rllib.env.vector_env.VectorEnv
+  (`num_envs`, `observation_space`, `action_space`, `vector_reset()`, `reset_at()`,
+  `vector_step()`): actions [B,NA] in, flat observation rows [B,NA,9R+1] float32 / rewards [B,NA]
+  / dones [B] out, one wh_vector_step call per step, done episodes restarted on the device.
+* `WarehouseBaseEnv` -- the dict surface of ray.rllib.env.base_env.BaseEnv (`poll()`,
+  `send_actions()`, `try_reset()`), with per-agent ids str(i) like warehouse/core.py:248-260,
+  435-442, for samplers that speak MultiEnvDicts.  It does not auto-reset: like RLlib's
+  MultiAgentEnvWrapper, an env whose "__all__" is done waits for try_reset(env_id).
+
+Both report the on_episode_end metrics of scripts/train.py:18-23 from device counters
+(`custom_metrics()`).
+
+Observation rows are the gym Dict observation (warehouse/core.py:118-148) flattened the way a
+Dict-flattening preprocessor does: keys in sorted order, each value flattened row-major, as
+float32.  ray is not installed here, so that flat layout is "parity unpinned" against RLlib itself;
+every value is pinned against the reference's per-agent dicts (tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ._compat import spaces
+from ._geometry import GEOMETRY
+from .batched import BatchedWarehouse
+
+# sorted gym.spaces.Dict key order and each key's flattened width, R = num_requests
+OBS_KEYS = ("num_agents", "other_availabilities", "other_delivery_targets", "other_positions",
+            "requests", "self_availability", "self_delivery_target", "self_position")
+
+
+def obs_key_widths(R: int) -> Dict[str, int]:
+    return {"num_agents": 1, "other_availabilities": R - 1, "other_delivery_targets": 2 * (R - 1),
+            "other_positions": 2 * (R - 1), "requests": 4 * R, "self_availability": 1,
+            "self_delivery_target": 2, "self_position": 2}
+
+
+def flat_observation_space(R: int, D: int):
+    """Box of one flattened observation row, bounds taken from core.py:118-148."""
+    lo, hi = [], []
+    bounds = {"num_agents": (1, R), "other_availabilities": (0, 1), "other_delivery_targets": (0, D),
+              "other_positions": (0, D), "requests": (0, D), "self_availability": (0, 1),
+              "self_delivery_target": (0, D), "self_position": (0, D)}
+    for k, w in obs_key_widths(R).items():
+        lo += [bounds[k][0]] * w
+        hi += [bounds[k][1]] * w
+    return spaces.Box(low=np.array(lo, np.float32), high=np.array(hi, np.float32), shape=(9 * R + 1,),
+                      dtype=np.float32)
+
+
+def unflatten_row(row: np.ndarray, R: int) -> Dict[str, np.ndarray]:
+    """One flat row back to the reference's observation dict (core.py:248-260 / 421-432)."""
+    row = np.asarray(row)
+    out, o = {}, 0
+    shapes = {"num_agents": (1,), "other_availabilities": (R - 1,), "other_delivery_targets": (R - 1, 2),
+              "other_positions": (R - 1, 2), "requests": (R, 4), "self_availability": (1,),
+              "self_delivery_target": (2,), "self_position": (2,)}
+    for k, w in obs_key_widths(R).items():
+        dt = np.int8 if k in ("other_availabilities", "self_availability") else np.int32
+        out[k] = row[o:o + w].astype(dt).reshape(shapes[k])
+        o += w
+    return out
+
+
+class WarehouseVectorEnv:
+    """`num_envs` episodes of one variant as a vectorised sampler env (tensor API).  Train
+    variants (default, like scripts/train.py:11-15) draw each episode's agent count n on the
+    device; rows and rewards of slots >= n are zero and `agent_mask()` marks the live ones."""
+
+    def __init__(self, variant: str = "medium", num_envs: int = 1024, num_agents: Optional[int] = None,
+                 *, train: bool = True, seed: int = 0, env_offset: int = 0, device=None,
+                 autoreset: bool = True):
+        self.env = BatchedWarehouse(variant, num_envs, num_agents, train=train, seed=seed,
+                                    env_offset=env_offset, device=device)
+        geo = GEOMETRY[variant]
+        self.variant = variant
+        self.num_envs = self.env.B
+        self.num_agents = self.env.agent_slots
+        self.num_requests = geo["R"]
+        self.autoreset = bool(autoreset)
+        self.observation_space = flat_observation_space(geo["R"], geo["D"])
+        self.action_space = spaces.Discrete(9)
+        self.stats = self.env.enable_episode_stats()
+        self._slot = torch.arange(self.num_agents, device=self.env.device, dtype=torch.int32)
+
+    @property
+    def device(self):
+        return self.env.device
+
+    def vector_reset(self) -> torch.Tensor:
+        self.env.reset()
+        return self.env.observe()
+
+    def reset_at(self, index=None, mask=None) -> torch.Tensor:
+        """Restart env `index` (or every env in the [B] bool `mask`); returns the full obs tensor,
+        whose rows of the restarted envs are their first observations."""
+        if mask is None:
+            mask = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
+            mask[int(index)] = True
+        self.env.reset(mask=mask)
+        return self.env.observe()
+
+    def vector_step(self, actions, mask=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, dict]:
+        """actions [B,NA] int in 0..8 (values outside act as 4 = stay); `mask` [B] bool limits the
+        step to some envs.  Returns env-owned (obs [B,NA,9R+1], rewards [B,NA], dones [B] bool,
+        infos)."""
+        obs, rew, done = self.env.vector_step(actions, autoreset=self.autoreset, mask=mask)
+        return obs, rew, done.bool(), {}
+
+    def agent_mask(self) -> torch.Tensor:
+        """[B,NA] bool: slot i is a live agent of its env's current episode (i < n)."""
+        n = (self.env.state[0] >> 16) & 0xFF
+        return self._slot[None, :] < n[:, None]
+
+    def custom_metrics(self) -> Dict[str, Dict[str, float]]:
+        return self.stats.custom_metrics()
+
+
+class WarehouseBaseEnv:
+    """MultiEnvDict surface (ray.rllib.env.base_env.BaseEnv) over one batch on the device."""
+
+    def __init__(self, variant: str = "medium", num_envs: int = 4, num_agents: Optional[int] = None,
+                 *, train: bool = True, seed: int = 0, env_offset: int = 0, device=None):
+        self.vec = WarehouseVectorEnv(variant, num_envs, num_agents, train=train, seed=seed,
+                                      env_offset=env_offset, device=device, autoreset=False)
+        self.num_envs = self.vec.num_envs
+        self.observation_space = self.vec.observation_space
+        self.action_space = self.vec.action_space
+        obs = self.vec.vector_reset()
+        self._pending = self._pack(obs, None, None, range(self.num_envs))
+
+    def _pack(self, obs, rew, done, env_ids):
+        n = ((self.vec.env.state[0] >> 16) & 0xFF).cpu().numpy()
+        o = obs.cpu().numpy()
+        r = None if rew is None else rew.cpu().numpy()
+        d = None if done is None else done.cpu().numpy()
+        res = ({}, {}, {}, {}, {})
+        for e in env_ids:
+            ids = [str(i) for i in range(int(n[e]))]
+            res[0][e] = {a: o[e, i] for i, a in enumerate(ids)}
+            res[1][e] = {a: (0.0 if r is None else float(r[e, i])) for i, a in enumerate(ids)}
+            dd = bool(d[e]) if d is not None else False
+            res[2][e] = {**{a: dd for a in ids}, "__all__": dd}
+            res[3][e] = {a: {} for a in ids}
+            res[4][e] = {}
+        return res
+
+    def poll(self):
+        """(obs, rewards, dones, infos, off_policy_actions), each {env_id: {agent_id: value}},
+        for every env with results not yet polled."""
+        out, self._pending = self._pending, ({}, {}, {}, {}, {})
+        return out
+
+    def send_actions(self, action_dict: Dict[int, Dict[str, int]]) -> None:
+        """Step the envs named in `action_dict` (other envs are untouched; an agent missing from
+        its env's dict takes action 4 = stay).  Actions wrap like Python indexing (core.py:279-281)."""
+        acts = np.full((self.num_envs, self.vec.num_agents), 4, np.int32)
+        mask = np.zeros(self.num_envs, bool)
+        for e, ad in action_dict.items():
+            mask[e] = True
+            for a, v in ad.items():
+                v = int(v)
+                if not -9 <= v < 9:
+                    raise IndexError("list index out of range")   # MOVES[a], core.py:281
+                acts[e, int(a)] = v % 9
+        obs, rew, done, _ = self.vec.vector_step(acts, mask=mask)
+        self._pending = self._pack(obs, rew, done, sorted(action_dict))
+
+    def try_reset(self, env_id: int) -> Dict[str, np.ndarray]:
+        obs = self.vec.reset_at(env_id)
+        return self._pack(obs, None, None, [env_id])[0][env_id]
+
+    def get_sub_environments(self):
+        return []   # the envs live on the device as one batch, not as Python objects
+
+    def custom_metrics(self) -> Dict[str, Dict[str, float]]:
+        return self.vec.custom_metrics()
