@@ -10,6 +10,10 @@ policy+transition for every env; every step writes rewards [B,8] f32 and dones [
 nothing on the data path (no RCCL); a gloo group only aligns the timing window and takes the max.
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  alt_launch_mode -- the same workload as a hipGraph of one-step launches (state through HBM)
+  sampler_path -- the RLlib sampler route at the same B x NA: policy -> wh_vector_step (step +
+                  auto-reset + float32 observation rows), with the observation kernel's roofline
+                  (it writes B*NA*(9R+1)*4 bytes per step: HBM-write bound)
   roofline     -- algorithmic bytes of the step kernel / its mean duration (HIP events on the
                   launch stream), against the 8 TB/s HBM peak; `traffic` from the committed
                   rocprofv3 PMC summary (profiles/) when present.
@@ -159,6 +163,53 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist):
     return elapsed, kms[len(kms) // 2], spl
 
 
+def measure_sampler(env, K, W, dev, world, dist):
+    """The RLlib sampler route (scripts/train.py's workload): per step the device greedy policy
+    stands in for the learner's policy, then wh_vector_step = step + auto-reset + observation
+    rows [B,NA,9R+1] f32.  hipGraph of G steps.  Returns (elapsed_s, observe_kernel_ms)."""
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+
+    def one():
+        env.vector_step(env.policy("greedy", 0.0), autoreset=True, observe=True)
+
+    for _ in range(max(W, 3)):
+        one()
+    torch.cuda.synchronize(dev)
+    G = min(K, 100)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(G):
+            one()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(K // G):
+        graph.replay()
+    for _ in range(K % G):
+        one()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # observe kernel alone: 20 back-to-back launches between HIP events on the launch stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a, b in evs:
+        a.record(stream)
+        for _ in range(20):
+            env.observe()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kms = sorted(a.elapsed_time(b) / 20 for a, b in evs)
+    return elapsed, kms[len(kms) // 2]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -173,6 +224,7 @@ def main():
                          "graph: hipGraph of one-step launches, state round-trips HBM every step")
     ap.add_argument("--chunk", type=int, default=200)
     ap.add_argument("--no-alt", action="store_true", help="skip the other launch mode")
+    ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpus)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -211,6 +263,23 @@ def main():
                "roofline_frac": bpl2 / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
                "traffic": load_traffic(f"{args.variant}_n{NA}_{other}")}
 
+    sampler = None
+    if not args.no_sampler:
+        Ks = min(K, 1000)
+        el3, oms = measure_sampler(env, Ks, W, dev, world, dist)
+        obs_b = B * NA * env.obs_len * 4 + B * 4 * words     # rows written + packed state read
+        sampler = {
+            "workload": f"RLlib sampler route: device greedy actions -> wh_vector_step (step + auto-reset "
+                        f"+ f32 observation rows [B,{NA},{env.obs_len}]), hipGraph of 100 steps",
+            "value": world * B * NA * Ks / el3, "unit": "agent-steps/s", "steps": Ks,
+            "ms_per_step": el3 * 1e3 / Ks,
+            "roofline": {"bound": "hbm", "kernel": "k_observe", "kernel_ms": oms,
+                         "bytes_per_launch": obs_b, "achieved": obs_b / (oms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": obs_b / (oms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": load_traffic(f"{args.variant}_n{NA}_observe")},
+        }
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -248,6 +317,7 @@ def main():
                         "keeps state in registers and is VALU-issue bound (DESIGN.md, Roofline)",
             },
             "alt_launch_mode": alt,
+            "sampler_path": sampler,
         }
         if not args.no_cpu_baseline:
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)

@@ -714,7 +714,7 @@ struct StepParams {
 // on_episode_end metrics of scripts/train.py:18-23): one set of global atomics per distinct n in
 // the wave.  Sums, minima and maxima are built from ballots over bit slices, so only active lanes
 // contribute and the integer results do not depend on lane or wave order.
-__device__ __noinline__ void flush_episodes(bool fin, uint32_t n, uint32_t ret, const wh_episode_stats& st) {
+__device__ __forceinline__ void flush_episodes(bool fin, uint32_t n, uint32_t ret, const wh_episode_stats& st) {
   uint64_t pend = __ballot(fin);
   while (pend) {
     const int leader = __ffsll((unsigned long long)pend) - 1;
