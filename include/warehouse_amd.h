@@ -168,6 +168,31 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream);
 
+/* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a
+ * ReLU MLP, hidden_layer_sizes [256,256] Small / [512,512] Medium / [1024,256] Large, 9 action
+ * logits), i.e. trainer.compute_action(obs) of scripts/rollout.py:84-86 for every agent row of a
+ * batch.  bf16 MFMA with f32 accumulation; activations are rounded to bf16 between layers.
+ * Supported: in_dim = 9R+1 of a variant with its hidden sizes, out_dim = 9 (else WH_ENOTSUP). */
+typedef struct wh_mlp_desc {
+  int32_t in_dim, hidden0, hidden1, out_dim;
+} wh_mlp_desc;
+
+/* Size of the packed weight blob (device bytes).  Host only. */
+int wh_mlp_query(const wh_mlp_desc* d, int64_t* packed_bytes);
+
+/* Pack host f32 weights in torch nn.Linear layout (w0 [hidden0, in_dim], b0 [hidden0],
+ * w1 [hidden1, hidden0], b1 [hidden1], w2 [out_dim, hidden1], b2 [out_dim]) into the device blob
+ * `packed` (wh_mlp_query bytes, 16-byte aligned).  Synchronous. */
+int wh_mlp_pack(const wh_mlp_desc* d, const float* w0, const float* b0, const float* w1,
+                const float* b1, const float* w2, const float* b2, void* packed);
+
+/* obs [rows, in_dim] f32 -> logits [rows, 9] f32 and/or actions [rows] int32 (either may be NULL,
+ * not both).  explore = 0: argmax, first maximum wins; explore = 1: Gumbel-max sample of
+ * Categorical(logits), noise from philox (seed; counter row, step, purpose 5). */
+int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const float* obs,
+                   float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
+                   void* stream);
+
 /* Library build identification (e.g. "warehouse_amd gfx950 <date>"). */
 const char* wh_version(void);
 

@@ -27,6 +27,7 @@
 #include <string.h>
 #include <vector>
 
+#include "philox.h"
 #include "warehouse_amd.h"
 
 namespace {
@@ -68,21 +69,6 @@ __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast
 __device__ __forceinline__ uint32_t as_u(short2v v) { return __builtin_bit_cast(uint32_t, v); }
 
 // ----------------------------------------------------------------------------- small helpers
-__device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;   // one v_mad_u64_u32 each
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
-                   (uint32_t)p0);
-  }
-  return c;
-}
-
 __device__ __forceinline__ uint32_t comp(const uint4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }

@@ -29,7 +29,7 @@ WH_POLICY_RANDOM = 2
 
 # every symbol include/warehouse_amd.h declares
 SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observe", "wh_policy",
-           "wh_rollout", "wh_vector_step", "wh_version")
+           "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version")
 
 
 class WhConfig(ctypes.Structure):
@@ -73,6 +73,11 @@ class WhEpisodeStats(ctypes.Structure):
     ]
 
 
+class WhMlpDesc(ctypes.Structure):
+    _fields_ = [("in_dim", ctypes.c_int32), ("hidden0", ctypes.c_int32), ("hidden1", ctypes.c_int32),
+                ("out_dim", ctypes.c_int32)]
+
+
 class WarehouseNativeError(RuntimeError):
     pass
 
@@ -106,6 +111,10 @@ def lib() -> ctypes.CDLL:
     _ST = ctypes.POINTER(WhEpisodeStats)
     L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     L.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    _MD = ctypes.POINTER(WhMlpDesc)
+    L.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
+    L.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
+    L.wh_mlp_forward.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
     for name in SYMBOLS:
         if name != "wh_version":
             getattr(L, name).restype = ctypes.c_int

@@ -1,0 +1,113 @@
+"""GPU numerics of the SAC policy kernel (wh_mlp_forward) against a plain PyTorch reference of the
+same network (scripts/experiments/warehouse-*-sac policy_model shapes).
+
+Tolerances (stated here, checked below):
+  * logits vs the float64 reference that rounds weights, inputs and hidden activations to bf16
+    exactly where the kernel does: |d| <= 2e-3 + 2e-3 |ref|  (left: f32 accumulation order and the
+    rare bf16 rounding flip of a hidden unit).
+  * logits vs the plain fp32 network (no bf16 anywhere): |d| <= 3e-2 max|ref|  (the bf16 error).
+  * argmax actions equal the reference's wherever its top-2 margin exceeds 1e-2.
+  * explore=1 samples follow softmax(logits): chi-square over 9 bins below the 1e-4 quantile.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def wh():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    import warehouse
+    import warehouse.policy  # noqa: F401
+
+    return warehouse
+
+
+def reference_logits(w, x, bf16):
+    import torch
+
+    def q(a):
+        t = torch.as_tensor(np.asarray(a), dtype=torch.float32)
+        return (t.to(torch.bfloat16) if bf16 else t).to(torch.float64)
+
+    h = q(x)
+    h = torch.relu(h @ q(w["w0"]).T + torch.as_tensor(w["b0"], dtype=torch.float64))
+    h = q(h.to(torch.float32)) if bf16 else h
+    h = torch.relu(h @ q(w["w1"]).T + torch.as_tensor(w["b1"], dtype=torch.float64))
+    h = q(h.to(torch.float32)) if bf16 else h
+    return (h @ q(w["w2"]).T + torch.as_tensor(w["b2"], dtype=torch.float64)).numpy()
+
+
+def observation_rows(wh, variant, na, B, extra_random):
+    import torch
+
+    env = wh.BatchedWarehouse(variant, B, na, seed=4)
+    env.reset()
+    env.rollout(23, "greedy", 0.1)
+    rows = env.observe().reshape(-1, env.obs_len)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    rnd = (torch.randn((extra_random, env.obs_len), generator=g) * 6).to(rows.device)
+    return torch.cat([rows, rnd]).contiguous()
+
+
+@pytest.mark.parametrize("variant,na", [("small", 4), ("medium", 8), ("large", 16)])
+def test_mlp_logits_and_argmax_vs_torch(wh, variant, na):
+    net = wh.policy.MLPPolicy(variant, seed=11)
+    x = observation_rows(wh, variant, na, 61, 203)          # ragged row count
+    acts, lg = net(x, logits=True)
+    lg, acts = lg.cpu().numpy(), acts.cpu().numpy()
+    xc = x.cpu().numpy()
+    ref = reference_logits(net.weights, xc, bf16=True)
+    np.testing.assert_array_less(np.abs(lg - ref), 2e-3 + 2e-3 * np.abs(ref))
+    ref32 = reference_logits(net.weights, xc, bf16=False)
+    assert np.abs(lg - ref32).max() <= 3e-2 * np.abs(ref32).max()
+    srt = np.sort(ref, axis=1)
+    clear = srt[:, -1] - srt[:, -2] > 1e-2
+    assert clear.mean() > 0.9
+    np.testing.assert_array_equal(acts[clear], ref.argmax(1)[clear])
+    # actions-only launch gives the same argmax
+    a2, none = net(x)
+    assert none is None
+    np.testing.assert_array_equal(a2.cpu().numpy(), acts)
+
+
+def test_mlp_explore_samples_softmax(wh):
+    import torch
+
+    net = wh.policy.MLPPolicy("medium", seed=3)
+    x = observation_rows(wh, "medium", 8, 1, 0)[:1]
+    rows = 1 << 17
+    xx = x.expand(rows, -1).contiguous()
+    _, lg = net(xx[:1], logits=True)
+    p = torch.softmax(lg[0].double(), 0).cpu().numpy()
+    acts, _ = net(xx, explore=True, seed=9, step=5)
+    cnt = np.bincount(acts.cpu().numpy(), minlength=9)
+    exp = p * rows
+    chi2 = ((cnt - exp) ** 2 / exp).sum()
+    assert chi2 < 37.0      # chi-square, 8 dof, p = 1e-5
+    acts2, _ = net(xx, explore=True, seed=9, step=5)
+    np.testing.assert_array_equal(acts.cpu().numpy(), acts2.cpu().numpy())      # counter-based: reproducible
+    acts3, _ = net(xx, explore=True, seed=9, step=6)
+    assert (acts3.cpu().numpy() != acts.cpu().numpy()).any()
+
+
+def test_mlp_edge_cases(wh):
+    import ctypes
+
+    import torch
+    from warehouse import _native as nat
+
+    net = wh.policy.MLPPolicy("small", seed=1)
+    empty = torch.empty((0, net.in_dim), device=net.device)
+    a, _ = net(empty)
+    assert a.numel() == 0
+    one = torch.zeros((1, net.in_dim), device=net.device)
+    _, lg = net(one, logits=True)
+    ref = reference_logits(net.weights, np.zeros((1, net.in_dim), np.float32), bf16=True)
+    np.testing.assert_allclose(lg.cpu().numpy(), ref, atol=2e-3, rtol=2e-3)
+    bad = nat.WhMlpDesc(net.in_dim, 128, 128, 9)
+    assert nat.lib().wh_mlp_forward(ctypes.byref(bad), net.packed.data_ptr(), 1, one.data_ptr(), None,
+                                    None, 0, 0, 0, None) == nat.WH_ENOTSUP

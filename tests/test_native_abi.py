@@ -78,3 +78,24 @@ def test_no_cpu_fallback():
         warehouse.BatchedWarehouse("small", 4, 2)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         warehouse.WarehouseSmall(2)
+
+
+def test_mlp_query_shapes():
+    """wh_mlp_query: the three SAC policy_model shapes (scripts/experiments/warehouse-*-sac) and
+    nothing else; host only."""
+    import ctypes
+
+    from warehouse import _native
+
+    lib = _native.lib()
+    n = ctypes.c_int64()
+    for (i, h0, h1) in ((37, 256, 256), (82, 512, 512), (145, 1024, 256)):
+        d = _native.WhMlpDesc(i, h0, h1, 9)
+        assert lib.wh_mlp_query(ctypes.byref(d), ctypes.byref(n)) == _native.WH_OK
+        kq = (i + 15) // 16
+        frags = (h0 // 32) * kq * 64 + (h1 // 32) * (h0 // 32) * 128 + (h1 // 32) * 128
+        assert n.value == frags * 16 + 4 * (h0 + h1 + 32)
+    for bad in ((82, 512, 256, 9), (82, 512, 512, 4), (40, 256, 256, 9)):
+        d = _native.WhMlpDesc(*bad)
+        assert lib.wh_mlp_query(ctypes.byref(d), ctypes.byref(n)) == _native.WH_ENOTSUP
+    assert lib.wh_mlp_query(None, ctypes.byref(n)) == _native.WH_EINVAL
