@@ -14,6 +14,9 @@ Rank 0 prints ONE JSON line.  Besides the contract fields it carries
   sampler_path -- the RLlib sampler route at the same B x NA: policy -> wh_vector_step (step +
                   auto-reset + float32 observation rows), with the observation kernel's roofline
                   (it writes B*NA*(9R+1)*4 bytes per step: HBM-write bound)
+  policy_path  -- scripts/rollout.py's loop with the SAC policy network on the device
+                  (wh_mlp_forward over all agent rows, then wh_vector_step), with the MLP kernel's
+                  MFMA roofline (dense bf16 peak)
   roofline     -- algorithmic bytes of the step kernel / its mean duration (HIP events on the
                   launch stream), against the 8 TB/s HBM peak; `traffic` from the committed
                   rocprofv3 PMC summary (profiles/) when present.
@@ -35,6 +38,7 @@ for _p in (ROOT, os.path.join(ROOT, "rllib-warehouse_amd")):
 
 METRIC = "agent-steps/sec (aggregate) at B=65536 envs × 8 agents, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
+MFMA_BF16_PEAK_TFS = 2500.0   # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 
 
 def cpu_worker(args):
@@ -210,6 +214,59 @@ def measure_sampler(env, K, W, dev, world, dist):
     return elapsed, kms[len(kms) // 2]
 
 
+def measure_policy(env, K, W, dev, world, dist):
+    """scripts/rollout.py's loop on the device: per step the SAC policy network
+    (wh_mlp_forward, argmax) over all B x NA observation rows, then wh_vector_step (step +
+    auto-reset + next rows).  hipGraph of G steps.  Returns (elapsed_s, mlp_kernel_ms, net)."""
+    import torch
+
+    import warehouse.policy as wp
+
+    net = wp.MLPPolicy(env.variant, seed=7, device=dev)
+    B, NA = env.B, env.agent_slots
+    acts = torch.empty((B, NA), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    obs = env.observe()
+
+    def one():
+        net(obs.view(B * NA, -1), step=0, actions=acts.view(-1))
+        env.vector_step(acts, autoreset=True, observe=True)
+
+    for _ in range(max(min(W, 20), 3)):
+        one()
+    torch.cuda.synchronize(dev)
+    G = min(K, 20)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(G):
+            one()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(K // G):
+        graph.replay()
+    for _ in range(K % G):
+        one()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a, b in evs:
+        a.record(stream)
+        for _ in range(5):
+            net(obs.view(B * NA, -1), step=0, actions=acts.view(-1))
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kms = sorted(a.elapsed_time(b) / 5 for a, b in evs)
+    return elapsed, kms[len(kms) // 2], net
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,6 +282,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=200)
     ap.add_argument("--no-alt", action="store_true", help="skip the other launch mode")
     ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
+    ap.add_argument("--no-policy", action="store_true", help="skip the SAC-policy rollout measurement")
+    ap.add_argument("--policy-steps", type=int, default=200)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpus)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -280,6 +339,24 @@ def main():
                          "traffic": load_traffic(f"{args.variant}_n{NA}_observe")},
         }
 
+    policy_line = None
+    if not args.no_policy:
+        Kp = min(K, args.policy_steps)
+        el4, mms, net = measure_policy(env, Kp, W, dev, world, dist)
+        rows = B * NA
+        flop = 2.0 * rows * (net.in_dim * net.hidden[0] + net.hidden[0] * net.hidden[1] + net.hidden[1] * 9)
+        policy_line = {
+            "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
+                        f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset + "
+                        f"observation rows); random-init weights (no checkpoint ships with the reference)",
+            "value": world * B * NA * Kp / el4, "unit": "agent-steps/s", "steps": Kp,
+            "ms_per_step": el4 * 1e3 / Kp, "dtype": "bf16 MFMA, f32 accumulate",
+            "roofline": {"bound": "mfma", "kernel": "k_mlp", "kernel_ms": mms, "flop_per_launch": flop,
+                         "achieved": flop / (mms * 1e-3) / 1e12, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": flop / (mms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS,
+                         "traffic": load_traffic(f"{args.variant}_n{NA}_mlp")},
+        }
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -318,6 +395,7 @@ def main():
             },
             "alt_launch_mode": alt,
             "sampler_path": sampler,
+            "policy_path": policy_line,
         }
         if not args.no_cpu_baseline:
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)

@@ -43,14 +43,19 @@ struct Net {
   static constexpr int IN = IN_, INP = (IN_ + 15) / 16 * 16, H0 = H0_, H1 = H1_, CH = CH_;
   static constexpr int KQ0 = INP / 16;        // layer-0 k-steps
   static constexpr int T0 = H0 / 32, T1 = H1 / 32;
+  static constexpr int NC = T0 / CH;          // chunks of layer-0 tiles
   static constexpr int OUT = 9;
-  // packed blob, in 16-byte fragments: W0 [T0][KQ0][64], W1 [T1][T0][2][64], W2 [T1][2][64],
-  // then f32 biases b0[H0], b1[H1], b2[32]
-  static constexpr int64_t W0F = (int64_t)T0 * KQ0 * 64;
-  static constexpr int64_t W1F = (int64_t)T1 * T0 * 2 * 64;
-  static constexpr int64_t W2F = (int64_t)T1 * 2 * 64;
-  static constexpr int64_t BYTES = (W0F + W1F + W2F) * 16 + 4 * (H0 + H1 + 32);
+  // packed blob, in MFMA A operands (64 lanes x 16 B = 1 KiB each):
+  //   NC chunks of { W0 [CH][KQ0], W1 [T1][CH][2] }   (one contiguous LDS stage each)
+  //   W2 [T1][2], then f32 biases b0[H0], b1[H1], b2[32]
+  static constexpr int CW0 = CH * KQ0, CW1 = T1 * CH * 2, COPS = CW0 + CW1;
+  static constexpr int64_t CHUNKS_OPS = (int64_t)NC * COPS;
+  static constexpr int64_t W2_OPS = (int64_t)T1 * 2;
+  static constexpr int64_t BIAS_OFF = (CHUNKS_OPS + W2_OPS) * 1024;
+  static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
+  static constexpr int LDS_BYTES = 2 * COPS * 1024 + 4 * (H0 + H1);
   static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % CH == 0, "tile shapes");
+  static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + biases must fit the 160 KiB LDS");
 };
 
 struct MlpArgs {
@@ -72,7 +77,7 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // bias + ReLU on a 32x32 accumulator tile whose rows start at hidden unit `base`, then the two
 // bf16 B-operand fragments (k-steps s = 0, 1) of the next layer.  Accumulator register g of lane
 // half h holds row (g&3) + 8(g>>2) + 4h.
-__device__ __forceinline__ void relu_to_frags(f32x16 t, const float* __restrict__ bias, int base, int h,
+__device__ __forceinline__ void relu_to_frags(f32x16 t, const float* bias, int base, int h,
                                               bf16x8& f0, bf16x8& f1) {
 #pragma unroll
   for (int G = 0; G < 4; ++G) {
@@ -90,23 +95,35 @@ __device__ __forceinline__ void relu_to_frags(f32x16 t, const float* __restrict_
   f1 = __builtin_convertvector(hi, bf16x8);
 }
 
+// One chunk of packed weights (COPS operands) global -> LDS stage by LDS-DMA: each wave copies
+// every 4th operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
+template <class N>
+__device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4* dst, int w, int lane) {
+#pragma unroll
+  for (int o = w; o < N::COPS; o += MT / 64)
+    __builtin_amdgcn_global_load_lds(src + o * 64 + lane, dst + o * 64, 16, 0, 0);
+}
+
 template <class N>
 __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // two weight stages (double buffer) + both hidden biases; A fragments are ds_read_b128 at
+  // operand*1 KiB + lane*16: conflict-free, and each 1 KiB operand is read by all 4 waves
+  __shared__ __attribute__((aligned(16))) u32x4 stage[2][N::COPS * 64];
+  __shared__ __attribute__((aligned(16))) float bias[N::H0 + N::H1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (LDS-DMA base in m0)
   const int r = lane & 31, h = lane >> 5;
   const int64_t s0 = ((int64_t)blockIdx.x * (MT / 64) + w) * 32;
-  if (s0 >= a.rows) return;                       // whole wave past the end
   const int64_t row = s0 + r;
-  const bool live = row < a.rows;
-  const u32x4* W0 = static_cast<const u32x4*>(a.packed);
-  const u32x4* W1 = W0 + N::W0F;
-  const u32x4* W2 = W1 + N::W1F;
-  const float* b0 = reinterpret_cast<const float*>(W2 + N::W2F);
-  const float* b1 = b0 + N::H0;
-  const float* b2 = b1 + N::H1;
+  const bool live = row < a.rows;                 // (a wave past the end still joins the barriers)
+  const u32x4* chunks = static_cast<const u32x4*>(a.packed);
+  const u32x4* W2 = chunks + N::CHUNKS_OPS * 64;
+  const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
+  const float* b2 = gb + N::H0 + N::H1;
 
-  // X^T as layer-0 B fragments: lane (r, h) holds obs[row][16q + 8h + j]
-  bf16x8 xb[N::KQ0];
+  // plain global loads first (biases, observation rows), then the LDS-DMA pipeline
+  for (int i = tid; i < N::H0 + N::H1; i += MT) bias[i] = gb[i];
+  bf16x8 xb[N::KQ0];                              // X^T fragments: lane (r,h) holds obs[row][16q+8h+j]
   const float* x = a.obs + (live ? row : 0) * N::IN;
 #pragma unroll
   for (int q = 0; q < N::KQ0; ++q) {
@@ -114,37 +131,62 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 16 * q + 8 * h + j;
-      v[j] = (live && k < N::IN) ? x[k] : 0.0f;
+      const float xv = x[k < N::IN ? k : N::IN - 1];        // branch-free: clamp, then select
+      v[j] = (live && k < N::IN) ? xv : 0.0f;
     }
     xb[q] = __builtin_convertvector(v, bf16x8);
   }
+  stage_chunk<N>(chunks, stage[0], w, lane);
+  __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): chunk 0 landed
+  __syncthreads();
 
   f32x16 t1[N::T1];
 #pragma unroll
   for (int n = 0; n < N::T1; ++n) t1[n] = f32x16{};
-  for (int c = 0; c < N::T0; c += N::CH) {
+  for (int c = 0; c < N::NC; ++c) {
+    if (c + 1 < N::NC) stage_chunk<N>(chunks + (int64_t)(c + 1) * N::COPS * 64, stage[(c + 1) & 1], w, lane);
+    const u32x4* S = stage[c & 1];
     bf16x8 hb[N::CH][2];
 #pragma unroll
     for (int m = 0; m < N::CH; ++m) {
       f32x16 t0{};
 #pragma unroll
-      for (int q = 0; q < N::KQ0; ++q) t0 = mfma(frag(W0 + ((int64_t)(c + m) * N::KQ0 + q) * 64 + lane), xb[q], t0);
-      relu_to_frags(t0, b0, 32 * (c + m), h, hb[m][0], hb[m][1]);
+      for (int q = 0; q < N::KQ0; ++q) t0 = mfma(frag(S + (m * N::KQ0 + q) * 64 + lane), xb[q], t0);
+      relu_to_frags(t0, bias, 32 * (c * N::CH + m), h, hb[m][0], hb[m][1]);
     }
+    // layer 1: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and B = hb[m][s].  A fragments
+    // are read from LDS one group of GS ahead of their MFMAs; the sched_barrier keeps the
+    // compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would spill).
+    constexpr int GS = 8, NG = N::CW1 / GS;
+    static_assert(N::CW1 % GS == 0, "layer-1 operand groups");
+    bf16x8 cur[GS], nxt[GS];
 #pragma unroll
-    for (int n = 0; n < N::T1; ++n)
+    for (int i = 0; i < GS; ++i) cur[i] = frag(S + (N::CW0 + i) * 64 + lane);
 #pragma unroll
-      for (int m = 0; m < N::CH; ++m)
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-          t1[n] = mfma(frag(W1 + (((int64_t)n * N::T0 + c + m) * 2 + s) * 64 + lane), hb[m][s], t1[n]);
+        for (int i = 0; i < GS; ++i) nxt[i] = frag(S + (N::CW0 + (g + 1) * GS + i) * 64 + lane);
+      }
+#pragma unroll
+      for (int i = 0; i < GS; ++i) {
+        const int op = g * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
+        t1[n] = mfma(cur[i], hb[m][s], t1[n]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < GS; ++i) cur[i] = nxt[i];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);           // next chunk landed
+    __syncthreads();                              // ... and nobody still reads the stage it reuses
   }
+  if (!live && s0 >= a.rows) return;
 
   f32x16 lg{};
 #pragma unroll
   for (int n = 0; n < N::T1; ++n) {
     bf16x8 f0, f1;
-    relu_to_frags(t1[n], b1, 32 * n, h, f0, f1);
+    relu_to_frags(t1[n], bias + N::H0, 32 * n, h, f0, f1);
     lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
     lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
   }
@@ -170,10 +212,16 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
   int arg = 0;
   if (a.explore) {
     // Gumbel-max: argmax(z + g), g = -log(-log u), u in (0,1) from philox(row, step)
-    const uint4 b0w = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, PUR_MLP << 24), a.k0, a.k1);
-    const uint4 b1w = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | 1u), a.k0, a.k1);
-    const uint4 b2w = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | 2u), a.k0, a.k1);
-    const uint32_t u32[12] = {b0w.x, b0w.y, b0w.z, b0w.w, b1w.x, b1w.y, b1w.z, b1w.w, b2w.x, b2w.y, b2w.z, b2w.w};
+    uint32_t u32[12];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
+                               a.k0, a.k1);
+      u32[4 * b] = v.x;
+      u32[4 * b + 1] = v.y;
+      u32[4 * b + 2] = v.z;
+      u32[4 * b + 3] = v.w;
+    }
 #pragma unroll
     for (int o = 0; o < N::OUT; ++o) {
       const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
@@ -203,32 +251,34 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
   uint16_t* f = reinterpret_cast<uint16_t*>(blob.data());
   // operand `op` = one MFMA A operand = 64 lanes x 8 bf16; the kernel reads lane l's 16 bytes
   auto put = [&](int64_t op, int lane, int j, float v) { f[(op * 64 + lane) * 8 + j] = to_bf16(v); };
-  // W0 [H0][IN]: natural k order (X^T fragments come from memory)
-  for (int m = 0; m < N::T0; ++m)
-    for (int q = 0; q < N::KQ0; ++q)
-      for (int l = 0; l < 64; ++l)
-        for (int j = 0; j < 8; ++j) {
-          const int k = 16 * q + 8 * (l >> 5) + j;
-          put((int64_t)m * N::KQ0 + q, l, j, k < N::IN ? w0[(int64_t)(32 * m + (l & 31)) * N::IN + k] : 0.0f);
-        }
-  // W1 [H1][H0], W2 [9][H1]: k order of an accumulator-as-operand fragment
+  // k order of an accumulator-as-operand fragment (layers 1, 2)
   auto kperm = [](int i, int s, int l, int j) { return 32 * i + 16 * s + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3); };
-  int64_t o1 = N::W0F / 64;                // operand (64-lane fragment) index of W1
-  for (int n = 0; n < N::T1; ++n)
-    for (int i = 0; i < N::T0; ++i)
-      for (int s = 0; s < 2; ++s)
+  for (int c = 0; c < N::NC; ++c) {
+    const int64_t base = (int64_t)c * N::COPS;
+    for (int m = 0; m < N::CH; ++m) {
+      const int t = c * N::CH + m;               // layer-0 row tile
+      for (int q = 0; q < N::KQ0; ++q)           // W0 [H0][IN], natural k order (X^T from memory)
         for (int l = 0; l < 64; ++l)
-          for (int j = 0; j < 8; ++j)
-            put(o1 + ((int64_t)n * N::T0 + i) * 2 + s, l, j, w1[(int64_t)(32 * n + (l & 31)) * N::H0 + kperm(i, s, l, j)]);
-  int64_t o2 = (N::W0F + N::W1F) / 64;
-  for (int i = 0; i < N::T1; ++i)
+          for (int j = 0; j < 8; ++j) {
+            const int k = 16 * q + 8 * (l >> 5) + j;
+            put(base + m * N::KQ0 + q, l, j, k < N::IN ? w0[(int64_t)(32 * t + (l & 31)) * N::IN + k] : 0.0f);
+          }
+      for (int n = 0; n < N::T1; ++n)            // W1 [H1][H0]
+        for (int s = 0; s < 2; ++s)
+          for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j)
+              put(base + N::CW0 + (n * N::CH + m) * 2 + s, l, j,
+                  w1[(int64_t)(32 * n + (l & 31)) * N::H0 + kperm(t, s, l, j)]);
+    }
+  }
+  for (int i = 0; i < N::T1; ++i)                // W2 [9][H1], rows padded to 32 with zeros
     for (int s = 0; s < 2; ++s)
       for (int l = 0; l < 64; ++l)
         for (int j = 0; j < 8; ++j) {
           const int o = l & 31;
-          put(o2 + (int64_t)i * 2 + s, l, j, o < N::OUT ? w2[(int64_t)o * N::H1 + kperm(i, s, l, j)] : 0.0f);
+          put(N::CHUNKS_OPS + i * 2 + s, l, j, o < N::OUT ? w2[(int64_t)o * N::H1 + kperm(i, s, l, j)] : 0.0f);
         }
-  float* bias = reinterpret_cast<float*>(blob.data() + (N::W0F + N::W1F + N::W2F) * 16);
+  float* bias = reinterpret_cast<float*>(blob.data() + N::BIAS_OFF);
   memcpy(bias, b0, 4 * N::H0);
   memcpy(bias + N::H0, b1, 4 * N::H1);
   memcpy(bias + N::H0 + N::H1, b2, 4 * N::OUT);
@@ -253,7 +303,7 @@ const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   static const MlpKernel reg[] = {
       make_mlp<37, 256, 256, 4>(),     // Small:  obs 9*4+1,  [256, 256]
       make_mlp<82, 512, 512, 2>(),     // Medium: obs 9*9+1,  [512, 512]
-      make_mlp<145, 1024, 256, 8>(),   // Large:  obs 9*16+1, [1024, 256]
+      make_mlp<145, 1024, 256, 2>(),   // Large:  obs 9*16+1, [1024, 256]
   };
   if (!d || d->out_dim != 9) return nullptr;
   for (const auto& k : reg)

@@ -117,6 +117,7 @@ class BatchedWarehouse:
                  geometry: Optional[dict] = None):
         geo = dict(GEOMETRY[variant] if geometry is None else geometry)
         self.geometry = geo
+        self.variant = variant if geometry is None else None
         self.train = bool(train)
         nmax = int(geo["max_agents"])
         slots = nmax if train or num_agents is None else int(num_agents)

@@ -84,3 +84,21 @@ class MLPPolicy:
         return actions, (logits if torch.is_tensor(logits) else None)
 
     __call__ = forward
+
+
+def policy_rollout(env, net: MLPPolicy, steps: int, *, explore: bool = False, seed: int = 0,
+                   first_step: int = 0, record=None):
+    """scripts/rollout.py's loop (compute_action per agent -> env.step, until done) for every env
+    of a BatchedWarehouse, on the device: per step one wh_mlp_forward over all B x NA observation
+    rows, then one wh_vector_step (step + auto-reset + the next observation rows).  `record`, if
+    given, is called as record(step, actions, rewards, dones) with env-owned device tensors.
+    Returns the obs tensor of the last step."""
+    obs = env.observe()
+    B, NA = env.B, env.agent_slots
+    acts = torch.empty((B, NA), dtype=torch.int32, device=env.device)
+    for s in range(steps):
+        net(obs.view(B * NA, -1), explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
+        obs, rew, done = env.vector_step(acts, autoreset=True, observe=True)
+        if record is not None:
+            record(s, acts, rew, done)
+    return obs

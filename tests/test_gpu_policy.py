@@ -111,3 +111,39 @@ def test_mlp_edge_cases(wh):
     bad = nat.WhMlpDesc(net.in_dim, 128, 128, 9)
     assert nat.lib().wh_mlp_forward(ctypes.byref(bad), net.packed.data_ptr(), 1, one.data_ptr(), None,
                                     None, 0, 0, 0, None) == nat.WH_ENOTSUP
+
+
+def test_policy_rollout_transitions_vs_oracle(wh):
+    """The device policy loop (wh_mlp_forward -> wh_vector_step with auto-reset) for 230 steps:
+    actions equal a separate forward on the same rows, and every transition equals the oracle's
+    given those actions (philox draws)."""
+    import torch
+
+    from oracle import batched as ob
+    from oracle import core as oc
+
+    B, na, seed = 512, 8, 17
+    L = oc.layout_for("medium")
+    env = wh.BatchedWarehouse("medium", B, na, seed=seed)
+    env.reset()
+    net = wh.policy.MLPPolicy("medium", seed=2)
+    S = ob.BState.zeros(L, B, na)
+    d = ob.PhiloxDraws(seed, np.arange(B))
+    ob.reset(L, S, d)
+    log = []
+
+    def record(s, acts, rew, done):
+        log.append((acts.cpu().numpy().copy(), rew.cpu().numpy().copy(), done.cpu().numpy().copy()))
+
+    obs0 = env.observe().clone()
+    ref_a0, _ = net(obs0.view(B * na, -1), explore=True, seed=1, step=0)
+    wh.policy.policy_rollout(env, net, 230, explore=True, seed=1, record=record)
+    np.testing.assert_array_equal(log[0][0].reshape(-1), ref_a0.cpu().numpy())
+    for s, (a, rew, done) in enumerate(log):
+        orew, odone, _, _ = ob.step(L, S, a, d)
+        np.testing.assert_array_equal(rew, orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(done.astype(bool), odone)
+        if odone.any():
+            ob.reset(L, S, d, mask=odone)
+    np.testing.assert_array_equal(env.observe().cpu().numpy(), ob.observe(L, S))
+    assert len({int(x) for x in np.unique(np.concatenate([a.reshape(-1) for a, _, _ in log]))}) > 1
