@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 
@@ -38,23 +39,28 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int MT = 256;                 // threads per workgroup: 4 waves x 32 samples
 constexpr uint32_t PUR_MLP = 5;         // philox purpose (1-4 are the simulator's, philox.h)
 
-template <int IN_, int H0_, int H1_, int CH_>
+template <int IN_, int H0_, int H1_, int CH_, int PASSES_>
 struct Net {
   static constexpr int IN = IN_, INP = (IN_ + 15) / 16 * 16, H0 = H0_, H1 = H1_, CH = CH_;
   static constexpr int KQ0 = INP / 16;        // layer-0 k-steps
   static constexpr int T0 = H0 / 32, T1 = H1 / 32;
-  static constexpr int NC = T0 / CH;          // chunks of layer-0 tiles
+  static constexpr int NC = T0 / CH;          // chunks of layer-0 tiles per pass
+  // Layer-1 rows are produced in PASSES passes of T1P tiles (layer 0 is recomputed per pass), so
+  // the live accumulators are T1P x 16 registers: at H1 = 512 one pass would need all 256 AGPRs
+  // and the rest of the loop would spill.
+  static constexpr int PASSES = PASSES_, T1P = T1 / PASSES_;
   static constexpr int OUT = 9;
   // packed blob, in MFMA A operands (64 lanes x 16 B = 1 KiB each):
-  //   NC chunks of { W0 [CH][KQ0], W1 [T1][CH][2] }   (one contiguous LDS stage each)
+  //   PASSES x NC chunks of { W0 [CH][KQ0], W1 rows of the pass [T1P][CH][2] }  (one LDS stage each)
   //   W2 [T1][2], then f32 biases b0[H0], b1[H1], b2[32]
-  static constexpr int CW0 = CH * KQ0, CW1 = T1 * CH * 2, COPS = CW0 + CW1;
-  static constexpr int64_t CHUNKS_OPS = (int64_t)NC * COPS;
+  static constexpr int CW0 = CH * KQ0, CW1 = T1P * CH * 2, COPS = CW0 + CW1;
+  static constexpr int NCH = PASSES * NC;     // chunks in all
+  static constexpr int64_t CHUNKS_OPS = (int64_t)NCH * COPS;
   static constexpr int64_t W2_OPS = (int64_t)T1 * 2;
   static constexpr int64_t BIAS_OFF = (CHUNKS_OPS + W2_OPS) * 1024;
   static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
   static constexpr int LDS_BYTES = 2 * COPS * 1024 + 4 * (H0 + H1);
-  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % CH == 0, "tile shapes");
+  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % CH == 0 && T1 % PASSES == 0, "tile shapes");
   static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + biases must fit the 160 KiB LDS");
 };
 
@@ -66,6 +72,7 @@ struct MlpArgs {
   int32_t* actions;
   int32_t explore;
   uint32_t k0, k1, step;
+  int32_t ablate;   // timing experiments only (env WH_MLP_ABLATE): 1 = no staging in the loop
 };
 
 __device__ __forceinline__ bf16x8 frag(const u32x4* p) { return __builtin_bit_cast(bf16x8, *p); }
@@ -140,55 +147,60 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): chunk 0 landed
   __syncthreads();
 
-  f32x16 t1[N::T1];
-#pragma unroll
-  for (int n = 0; n < N::T1; ++n) t1[n] = f32x16{};
-  for (int c = 0; c < N::NC; ++c) {
-    if (c + 1 < N::NC) stage_chunk<N>(chunks + (int64_t)(c + 1) * N::COPS * 64, stage[(c + 1) & 1], w, lane);
-    const u32x4* S = stage[c & 1];
-    bf16x8 hb[N::CH][2];
-#pragma unroll
-    for (int m = 0; m < N::CH; ++m) {
-      f32x16 t0{};
-#pragma unroll
-      for (int q = 0; q < N::KQ0; ++q) t0 = mfma(frag(S + (m * N::KQ0 + q) * 64 + lane), xb[q], t0);
-      relu_to_frags(t0, bias, 32 * (c * N::CH + m), h, hb[m][0], hb[m][1]);
-    }
-    // layer 1: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and B = hb[m][s].  A fragments
-    // are read from LDS one group of GS ahead of their MFMAs; the sched_barrier keeps the
-    // compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would spill).
-    constexpr int GS = 8, NG = N::CW1 / GS;
-    static_assert(N::CW1 % GS == 0, "layer-1 operand groups");
-    bf16x8 cur[GS], nxt[GS];
-#pragma unroll
-    for (int i = 0; i < GS; ++i) cur[i] = frag(S + (N::CW0 + i) * 64 + lane);
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (g + 1 < NG) {
-#pragma unroll
-        for (int i = 0; i < GS; ++i) nxt[i] = frag(S + (N::CW0 + (g + 1) * GS + i) * 64 + lane);
-      }
-#pragma unroll
-      for (int i = 0; i < GS; ++i) {
-        const int op = g * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
-        t1[n] = mfma(cur[i], hb[m][s], t1[n]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < GS; ++i) cur[i] = nxt[i];
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);           // next chunk landed
-    __syncthreads();                              // ... and nobody still reads the stage it reuses
-  }
-  if (!live && s0 >= a.rows) return;
-
   f32x16 lg{};
+  for (int p = 0; p < N::PASSES; ++p) {
+    f32x16 t1[N::T1P];
 #pragma unroll
-  for (int n = 0; n < N::T1; ++n) {
-    bf16x8 f0, f1;
-    relu_to_frags(t1[n], bias + N::H0, 32 * n, h, f0, f1);
-    lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
-    lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
+    for (int n = 0; n < N::T1P; ++n) t1[n] = f32x16{};
+    for (int c = 0; c < N::NC; ++c) {
+      const int g = p * N::NC + c;                // chunk index
+      if (g + 1 < N::NCH && !(a.ablate & 1))
+        stage_chunk<N>(chunks + (int64_t)(g + 1) * N::COPS * 64, stage[(g + 1) & 1], w, lane);
+      const u32x4* S = stage[g & 1];
+      bf16x8 hb[N::CH][2];
+#pragma unroll
+      for (int m = 0; m < N::CH; ++m) {
+        f32x16 t0{};
+#pragma unroll
+        for (int q = 0; q < N::KQ0; ++q) t0 = mfma(frag(S + (m * N::KQ0 + q) * 64 + lane), xb[q], t0);
+        relu_to_frags(t0, bias, 32 * (c * N::CH + m), h, hb[m][0], hb[m][1]);
+      }
+      // layer 1: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and B = hb[m][s].  A
+      // fragments are read from LDS one group of GS ahead of their MFMAs; the sched_barrier keeps
+      // the compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would spill).
+      constexpr int GS = 8, NG = N::CW1 / GS;
+      static_assert(N::CW1 % GS == 0, "layer-1 operand groups");
+      bf16x8 cur[GS], nxt[GS];
+#pragma unroll
+      for (int i = 0; i < GS; ++i) cur[i] = frag(S + (N::CW0 + i) * 64 + lane);
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) {
+#pragma unroll
+          for (int i = 0; i < GS; ++i) nxt[i] = frag(S + (N::CW0 + (gi + 1) * GS + i) * 64 + lane);
+        }
+#pragma unroll
+        for (int i = 0; i < GS; ++i) {
+          const int op = gi * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
+          t1[n] = mfma(cur[i], hb[m][s], t1[n]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < GS; ++i) cur[i] = nxt[i];
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);         // next chunk landed
+      __syncthreads();                            // ... and nobody still reads the stage it reuses
+    }
+    // layer 2 over this pass's hidden tiles
+#pragma unroll
+    for (int nn = 0; nn < N::T1P; ++nn) {
+      const int n = p * N::T1P + nn;
+      bf16x8 f0, f1;
+      relu_to_frags(t1[nn], bias + N::H0, 32 * n, h, f0, f1);
+      lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
+      lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
+      __builtin_amdgcn_sched_barrier(0);          // one tile at a time: no hoisting of all tiles
+    }
   }
 
   // logit o of sample r: o 0-3 in lane r regs 0-3, o 4-7 in lane r+32 regs 0-3, o 8 in lane r reg 4
@@ -253,8 +265,9 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
   auto put = [&](int64_t op, int lane, int j, float v) { f[(op * 64 + lane) * 8 + j] = to_bf16(v); };
   // k order of an accumulator-as-operand fragment (layers 1, 2)
   auto kperm = [](int i, int s, int l, int j) { return 32 * i + 16 * s + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3); };
-  for (int c = 0; c < N::NC; ++c) {
-    const int64_t base = (int64_t)c * N::COPS;
+  for (int g = 0; g < N::NCH; ++g) {
+    const int p = g / N::NC, c = g % N::NC;
+    const int64_t base = (int64_t)g * N::COPS;
     for (int m = 0; m < N::CH; ++m) {
       const int t = c * N::CH + m;               // layer-0 row tile
       for (int q = 0; q < N::KQ0; ++q)           // W0 [H0][IN], natural k order (X^T from memory)
@@ -263,12 +276,12 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
             const int k = 16 * q + 8 * (l >> 5) + j;
             put(base + m * N::KQ0 + q, l, j, k < N::IN ? w0[(int64_t)(32 * t + (l & 31)) * N::IN + k] : 0.0f);
           }
-      for (int n = 0; n < N::T1; ++n)            // W1 [H1][H0]
+      for (int nn = 0; nn < N::T1P; ++nn)        // W1 [H1][H0], rows of pass p
         for (int s = 0; s < 2; ++s)
           for (int l = 0; l < 64; ++l)
             for (int j = 0; j < 8; ++j)
-              put(base + N::CW0 + (n * N::CH + m) * 2 + s, l, j,
-                  w1[(int64_t)(32 * n + (l & 31)) * N::H0 + kperm(t, s, l, j)]);
+              put(base + N::CW0 + (nn * N::CH + m) * 2 + s, l, j,
+                  w1[(int64_t)(32 * (p * N::T1P + nn) + (l & 31)) * N::H0 + kperm(t, s, l, j)]);
     }
   }
   for (int i = 0; i < N::T1; ++i)                // W2 [9][H1], rows padded to 32 with zeros
@@ -292,18 +305,18 @@ struct MlpKernel {
   std::vector<uint8_t> (*pack)(const float*, const float*, const float*, const float*, const float*, const float*);
 };
 
-template <int IN, int H0, int H1, int CH>
+template <int IN, int H0, int H1, int CH, int PASSES>
 MlpKernel make_mlp() {
-  using N = Net<IN, H0, H1, CH>;
+  using N = Net<IN, H0, H1, CH, PASSES>;
   return MlpKernel{IN, H0, H1, N::BYTES, k_mlp<N>, pack<N>};
 }
 
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml
   static const MlpKernel reg[] = {
-      make_mlp<37, 256, 256, 4>(),     // Small:  obs 9*4+1,  [256, 256]
-      make_mlp<82, 512, 512, 2>(),     // Medium: obs 9*9+1,  [512, 512]
-      make_mlp<145, 1024, 256, 2>(),   // Large:  obs 9*16+1, [1024, 256]
+      make_mlp<37, 256, 256, 4, 1>(),     // Small:  obs 9*4+1,  [256, 256]
+      make_mlp<82, 512, 512, 2, 2>(),     // Medium: obs 9*9+1,  [512, 512]
+      make_mlp<145, 1024, 256, 2, 1>(),   // Large:  obs 9*16+1, [1024, 256]
   };
   if (!d || d->out_dim != 9) return nullptr;
   for (const auto& k : reg)
@@ -341,8 +354,9 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
   if (rows < 0) return WH_EINVAL;
   if (rows == 0) return WH_OK;
   if (!packed || !obs || (!logits && !actions)) return WH_EINVAL;
+  const char* abl = getenv("WH_MLP_ABLATE");
   MlpArgs a{packed, rows, obs, logits, actions, explore ? 1 : 0, (uint32_t)(seed & 0xFFFFFFFFu),
-            (uint32_t)(seed >> 32), step};
+            (uint32_t)(seed >> 32), step, abl ? atoi(abl) : 0};
   const int64_t rows_per_wg = 32 * (MT / 64);
   hipLaunchKernelGGL(k->fwd, dim3((unsigned)((rows + rows_per_wg - 1) / rows_per_wg)), dim3(MT), 0,
                      (hipStream_t)stream, a);

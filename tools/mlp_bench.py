@@ -9,7 +9,9 @@ import warehouse  # noqa: E402
 import warehouse.policy as wp  # noqa: E402
 
 B = int(os.environ.get("MLP_B", 65536))
-for variant, na in (("small", 4), ("medium", 8), ("large", 16)):
+for abl, variant, na in [(a, v, n) for a in os.environ.get("MLP_ABLATE", "0").split(",")
+                         for v, n in (("small", 4), ("medium", 8), ("large", 16))]:
+    os.environ["WH_MLP_ABLATE"] = abl
     net = wp.MLPPolicy(variant, seed=1)
     rows = B * na
     x = torch.randn((rows, net.in_dim), device="cuda") * 4
@@ -27,5 +29,5 @@ for variant, na in (("small", 4), ("medium", 8), ("large", 16)):
     us = t0.elapsed_time(t1) / reps * 1e3
     h0, h1 = net.hidden
     flop = 2.0 * rows * (net.in_dim * h0 + h0 * h1 + h1 * 9)
-    print(f"{variant:6s} rows={rows:8d} [{net.in_dim},{h0},{h1},9] {us:9.1f} us  {flop / us / 1e6:7.1f} TFLOP/s",
+    print(f"ablate={abl} {variant:6s} rows={rows:8d} [{net.in_dim},{h0},{h1},9] {us:9.1f} us  {flop / us / 1e6:7.1f} TFLOP/s",
           flush=True)
