@@ -777,9 +777,9 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
                                   (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, a.ablate);
     if (a.phase != PH_REGEN) {
-      if (a.rewards) store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid,
-                                      a.mask != nullptr);
-      if (a.dones) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
+      if (a.rewards && !(a.ablate & 64))
+        store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid, a.mask != nullptr);
+      if (a.dones && !(a.ablate & 64)) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
       if (a.returns) {
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) ret += rew[i];
@@ -792,7 +792,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
         if (__any(done)) flush_episodes(done, (s.hdr >> 16) & 0xFFu, epr, a.stats);
         if (done) epr = 0;
       }
-      if (done && a.autoreset) reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
+      if (done && a.autoreset && !(a.ablate & 128)) reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
     }
   }
   if (a.returns) a.returns[e] += ret;
@@ -842,8 +842,6 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
 // 16 lanes per env, then writes the group's contiguous [16 env x na x L] float region as float4s.
 // Small workgroups keep many groups in flight per CU, so one group's image build overlaps the
 // others' streaming stores.
-constexpr int OBS_EB = 16;        // envs per workgroup
-constexpr int OBS_PARTS = BT / OBS_EB;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Image offset of output value f of agent row i (sorted-key order, see wh_observe).
@@ -886,7 +884,7 @@ constexpr ObsSrc<R, NAM> make_obs_src() {
 template <int R, int NAM>
 __constant__ ObsSrc<R, NAM> kObsSrc = make_obs_src<R, NAM>();
 
-template <class C>
+template <class C, int OBS_EB>
 struct ObsLds {
   static constexpr int IMG = (C::L + 3) & ~3;
   static constexpr int SRCW = ObsSrc<C::R, C::NAM>::W;
@@ -898,12 +896,13 @@ struct ObsLds {
   uint32_t dst[C::DP];           // delivery cell, x | y << 16
 };
 
-template <class C>
+template <class C, int OBS_EB>
 __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ state, int64_t B, int na,
                                                 const uint32_t* __restrict__ tables,
                                                 float* __restrict__ obs, int quads) {
-  __shared__ ObsLds<C> O;
-  constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C>::SRCW;
+  __shared__ ObsLds<C, OBS_EB> O;
+  constexpr int OBS_PARTS = BT / OBS_EB;
+  constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C, OBS_EB>::SRCW;
   constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
   const int tid = threadIdx.x;
   const uint32_t* srcg = &kObsSrc<C::R, C::NAM>.w[0][0];
@@ -1207,7 +1206,7 @@ struct Kernels {
   void (*step[3])(StepParams);
   void (*step_ordered)(StepParams);
   void (*reset)(ResetParams);
-  void (*observe)(const uint32_t*, int64_t, int, const uint32_t*, float*, int);
+  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int);   // 8 / 16 / 64 envs per WG
   int tblw, nv;
 };
 
@@ -1221,7 +1220,9 @@ Kernels make_kernels() {
   k.step[2] = k_step<C, POL_RANDOM, false>;
   k.step_ordered = k_step<C, POL_EXTERNAL, true>;
   k.reset = k_reset<C>;
-  k.observe = k_observe<C>;
+  k.observe[0] = k_observe<C, 8>;
+  k.observe[1] = k_observe<C, 16>;
+  k.observe[2] = k_observe<C, 64>;
   k.tblw = C::TBLW;
   k.nv = C::NV;
   return k;
@@ -1430,7 +1431,12 @@ int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* ob
   if (B == 0) return WH_OK;
   if (!state || !obs) return WH_EINVAL;
   const int quads = ((g.NA * (9 * g.R + 1)) % 4 == 0) && ((uintptr_t)obs % 16 == 0);
-  hipLaunchKernelGGL(k->observe, dim3((unsigned)((B + OBS_EB - 1) / OBS_EB)), dim3(BT), 0,
+  // envs per workgroup: ~40-75 KB of rows per group (measured: 64 for Small-4's 592 B/env rows,
+  // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
+  const int row_bytes = 4 * g.NA * (9 * g.R + 1);
+  const int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
+  const int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
+  hipLaunchKernelGGL(k->observe[sel], dim3((unsigned)((B + ebx - 1) / ebx)), dim3(BT), 0,
                      (hipStream_t)stream, state, B, g.NA, tab, obs, quads);
   return hip_err(hipGetLastError());
 }

@@ -1,5 +1,6 @@
 """Phase-ablation timing of the fused step kernel (timing only: results are wrong by design).
-WH_ABLATE bits: 1 policy, 2 move, 4 expiry, 8 pickup, 16 regeneration, 32 delivery."""
+WH_ABLATE bits: 1 policy, 2 move, 4 expiry, 8 pickup, 16 regeneration, 32 delivery, 64 reward/done
+stores, 128 auto-reset."""
 import os
 import sys
 import time
@@ -14,7 +15,7 @@ B, C = 65536, 200
 env = warehouse.BatchedWarehouse(variant, B, na, seed=1)
 rew = torch.zeros((C, B, na), device="cuda")
 dn = torch.zeros((C, B), dtype=torch.uint8, device="cuda")
-masks = [0, 1, 2, 4, 8, 16, 32, 1 | 16, 63]
+masks = [int(m) for m in os.environ.get("ABL_MASKS", "0,1,2,4,8,16,32,17,63,64,128,127,255").split(",")]
 res = {m: [] for m in masks}
 for rnd in range(5):
     for m in masks:

@@ -8,8 +8,7 @@ import torch  # noqa: E402
 import warehouse  # noqa: E402
 
 B = int(os.environ.get("OBS_B", 65536))
-for nt, variant, na in [(nt, v, a) for nt in ("0", "1") for v, a in (("small", 4), ("medium", 8), ("large", 16))]:
-    os.environ["WH_OBS_NT"] = nt
+for variant, na in (("small", 4), ("medium", 8), ("large", 16)):
     env = warehouse.BatchedWarehouse(variant, B, na, seed=3)
     env.reset()
     env.rollout(37, "greedy", 0.0)
@@ -27,5 +26,5 @@ for nt, variant, na in [(nt, v, a) for nt in ("0", "1") for v, a in (("small", 4
     torch.cuda.synchronize()
     us = t0.elapsed_time(t1) / reps * 1e3
     nbytes = obs.numel() * 4 + env.state.numel() * 4
-    print(f"nt={nt} {variant:6s} na={na:2d} observe {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "
+    print(f"{variant:6s} na={na:2d} observe {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "
           f"(rows {obs.numel() * 4 / 1e6:.1f} MB + state {env.state.numel() * 4 / 1e6:.1f} MB)", flush=True)
