@@ -329,3 +329,34 @@ def test_edge_empty_batch_and_bad_config(wh):
         nat.query(nat.make_config(12, 4, (4, 8), 5, 200, 200))   # agents > requests
     with pytest.raises(ValueError):
         nat.query(nat.make_config(12, 4, (4, 8), 2, 200, 300))   # W > 255 not representable
+
+
+def test_c5_eight_shards_equal_one_batch_of_524288(wh):
+    """Config 5 on one GPU: B = 524,288 Medium x 8 envs as ONE batch equals the 8 per-GPU shards of
+    65,536 (env_offset = rank * B) that bench.py runs on an 8-GPU node -- bit-exact state,
+    rewards and observation rows; plus request/timer invariants over all 524,288 envs."""
+    import torch
+
+    B, G, seed, K = 524288, 8, 5, 30
+    L = oc.layout_for("medium")
+    full = wh.BatchedWarehouse("medium", B, 8, seed=seed)
+    full.reset()
+    rew = torch.zeros((K, B, 8), device=full.device)
+    full.rollout(K, "greedy", 0.0, rewards=rew)
+    for g in range(G):
+        sh = wh.BatchedWarehouse("medium", B // G, 8, seed=seed, env_offset=g * (B // G))
+        sh.reset()
+        r = torch.zeros((K, B // G, 8), device=sh.device)
+        sh.rollout(K, "greedy", 0.0, rewards=r)
+        sl = slice(g * (B // G), (g + 1) * (B // G))
+        torch.testing.assert_close(sh.state, full.state[:, sl], rtol=0, atol=0)
+        torch.testing.assert_close(r, rew[:, sl], rtol=0, atol=0)
+        if g == G - 1:
+            torch.testing.assert_close(sh.observe(), full.observe()[sl], rtol=0, atol=0)
+        del sh, r
+    c = canon(full)
+    active = c["pickup_target"] >= 0
+    assert (active.sum(1) == L.R).all()
+    assert ((c["pickup_timer"] >= 0) == active).all()
+    assert c["pos"].min() >= 0 and c["pos"].max() < L.D
+    assert float(rew.sum()) > 0
