@@ -93,6 +93,23 @@ def load_traffic(tag):
         return None
 
 
+def load_issue(tag, steps_per_launch):
+    """VALU issue view of the step kernel from the committed SQ counters (tools/profile_round.sh
+    with SQ=1 -> profiles/pmc_traffic.json): per wave and env-step, VALU instructions and wave
+    quad-cycles; one wave issues at most one VALU per quad-cycle (MI355X_MICROARCH.md)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        sq = json.load(open(path))[tag]["sq"]
+        waves = sq["SQ_WAVES"]
+        valu = sq["SQ_INSTS_VALU"] / waves / steps_per_launch
+        cyc = sq["SQ_WAVE_CYCLES"] / waves / steps_per_launch
+        return {"valu_per_wave_step": valu, "wave_quad_cycles_per_step": cyc, "valu_issue_frac": valu / cyc,
+                "lds_per_wave_step": sq["SQ_INSTS_LDS"] / waves / steps_per_launch,
+                "source": f"profiles/pmc_traffic.json:{tag}.sq"}
+    except Exception:
+        return None
+
+
 def measure(env, mode, policy, K, W, chunk, dev, world, dist):
     """Time K steps of `mode`; returns (elapsed_s_max_over_ranks, kernel_ms, steps_per_launch)."""
     import torch
@@ -390,8 +407,10 @@ def main():
                 "steps_per_launch": spl,
                 "bytes_per_launch": bytes_per_launch,
                 "bytes_per_env_step": bytes_per_launch / B / spl,
+                "issue": load_issue(f"{args.variant}_n{NA}_{args.mode}", spl),
                 "note": "algorithmic bytes = 2 x packed state + per-step rewards/dones; the fused kernel "
-                        "keeps state in registers and is VALU-issue bound (DESIGN.md, Roofline)",
+                        "keeps state in registers and is VALU-issue bound (one wave per SIMD at B=65536): "
+                        "`issue` is its VALU issue rate against one wave's ceiling (DESIGN.md §5)",
             },
             "alt_launch_mode": alt,
             "sampler_path": sampler,
