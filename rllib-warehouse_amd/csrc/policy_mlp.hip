@@ -36,12 +36,14 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int MT = 256;                 // threads per workgroup: 4 waves x 32 samples
+constexpr int MT = 512;                 // threads per workgroup: 8 waves x 32 samples (2 per SIMD)
 constexpr uint32_t PUR_MLP = 5;         // philox purpose (1-4 are the simulator's, philox.h)
 
 template <int IN_, int H0_, int H1_, int CH_, int PASSES_>
 struct Net {
-  static constexpr int IN = IN_, INP = (IN_ + 15) / 16 * 16, H0 = H0_, H1 = H1_, CH = CH_;
+  // inputs padded to whole k-steps, with two spare columns IN, IN+1 = 1.0 carrying b0 as a
+  // bf16 hi + lo pair, so layer 0's bias is added inside the MFMA at ~f32 precision
+  static constexpr int IN = IN_, INP = (IN_ + 2 + 15) / 16 * 16, H0 = H0_, H1 = H1_, CH = CH_;
   static constexpr int KQ0 = INP / 16;        // layer-0 k-steps
   static constexpr int T0 = H0 / 32, T1 = H1 / 32;
   static constexpr int NC = T0 / CH;          // chunks of layer-0 tiles per pass
@@ -59,7 +61,8 @@ struct Net {
   static constexpr int64_t W2_OPS = (int64_t)T1 * 2;
   static constexpr int64_t BIAS_OFF = (CHUNKS_OPS + W2_OPS) * 1024;
   static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
-  static constexpr int LDS_BYTES = 2 * COPS * 1024 + 4 * (H0 + H1);
+  static constexpr int STAGES = 2;            // chunk g in use, chunk g+1 landing
+  static constexpr int LDS_BYTES = STAGES * COPS * 1024 + 4 * (H0 + H1);
   static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % CH == 0 && T1 % PASSES == 0, "tile shapes");
   static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + biases must fit the 160 KiB LDS");
 };
@@ -81,6 +84,15 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// ReLU after the bf16 rounding, on the packed bits: a bf16 with the sign bit set is a negative
+// int16, so v_pk_max_i16(x, 0) is max(x, +0) for two values per op (round(max(v,0)) ==
+// max(round(v),0) since rounding keeps the sign).
+__device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
+  return __builtin_bit_cast(bf16x8, __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), (s16x8){}));
+}
+
 // bias + ReLU on a 32x32 accumulator tile whose rows start at hidden unit `base`, then the two
 // bf16 B-operand fragments (k-steps s = 0, 1) of the next layer.  Accumulator register g of lane
 // half h holds row (g&3) + 8(g>>2) + 4h.
@@ -90,7 +102,7 @@ __device__ __forceinline__ void relu_to_frags(f32x16 t, const float* bias, int b
   for (int G = 0; G < 4; ++G) {
     const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + base + 8 * G + 4 * h);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) t[4 * G + e] = fmaxf(t[4 * G + e] + bv[e], 0.0f);
+    for (int e = 0; e < 4; ++e) t[4 * G + e] += bv[e];
   }
   f32x8 lo, hi;
 #pragma unroll
@@ -98,8 +110,20 @@ __device__ __forceinline__ void relu_to_frags(f32x16 t, const float* bias, int b
     lo[j] = t[j];
     hi[j] = t[8 + j];
   }
-  f0 = __builtin_convertvector(lo, bf16x8);
-  f1 = __builtin_convertvector(hi, bf16x8);
+  f0 = relu_bf16(__builtin_convertvector(lo, bf16x8));
+  f1 = relu_bf16(__builtin_convertvector(hi, bf16x8));
+}
+
+// Layer-0 tile (bias already inside the MFMA) -> the two bf16 B-operand fragments.
+__device__ __forceinline__ void relu_to_frags_nb(f32x16 t, bf16x8& f0, bf16x8& f1) {
+  f32x8 lo, hi;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lo[j] = t[j];
+    hi[j] = t[8 + j];
+  }
+  f0 = relu_bf16(__builtin_convertvector(lo, bf16x8));
+  f1 = relu_bf16(__builtin_convertvector(hi, bf16x8));
 }
 
 // One chunk of packed weights (COPS operands) global -> LDS stage by LDS-DMA: each wave copies
@@ -111,141 +135,189 @@ __device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4
     __builtin_amdgcn_global_load_lds(src + o * 64 + lane, dst + o * 64, 16, 0, 0);
 }
 
+// Layer-0 MFMAs of one chunk: t0[m] = W0 tile (c*CH + m) . X^T  (accumulators only, no ReLU yet).
+// All CH*KQ0 A fragments are read first (one LDS round trip for the chunk, not one per MFMA).
+template <class N>
+__device__ __forceinline__ void layer0(const u32x4* S, const bf16x8 (&xb)[N::KQ0], int lane, f32x16 (&t0)[N::CH]) {
+  bf16x8 a[N::CH][N::KQ0];
+#pragma unroll
+  for (int m = 0; m < N::CH; ++m)
+#pragma unroll
+    for (int q = 0; q < N::KQ0; ++q) a[m][q] = frag(S + (m * N::KQ0 + q) * 64 + lane);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < N::CH; ++m) {
+    t0[m] = f32x16{};
+#pragma unroll
+    for (int q = 0; q < N::KQ0; ++q) t0[m] = mfma(a[m][q], xb[q], t0[m]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Layer-1 MFMAs of one chunk: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and
+// B = hb[m][s].  A fragments are read from LDS one group of GS ahead of their MFMAs; the
+// sched_barrier keeps the compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would
+// spill).  `mid` runs once, between two MFMA groups half-way through (the next chunk's ReLU goes
+// there, so its VALU work issues under this chunk's MFMAs).
+template <class N, class Mid>
+__device__ __forceinline__ void layer1(const u32x4* S, const bf16x8 (&hb)[N::CH][2], int lane,
+                                       f32x16 (&t1)[N::T1P], Mid mid) {
+  constexpr int GS = 4, NG = N::CW1 / GS, DEPTH = 2;   // fragments read DEPTH groups ahead
+  static_assert(N::CW1 % GS == 0 && NG >= DEPTH, "layer-1 operand groups");
+  bf16x8 buf[DEPTH + 1][GS];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int i = 0; i < GS; ++i) buf[d][i] = frag(S + (N::CW0 + d * GS + i) * 64 + lane);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    if (gi + DEPTH < NG) {
+#pragma unroll
+      for (int i = 0; i < GS; ++i) buf[(gi + DEPTH) % (DEPTH + 1)][i] = frag(S + (N::CW0 + (gi + DEPTH) * GS + i) * 64 + lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);             // later groups' reads issue BEFORE this group's MFMAs
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int op = gi * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
+      t1[n] = mfma(buf[gi % (DEPTH + 1)][i], hb[m][s], t1[n]);
+    }
+    if (gi == NG / 2) mid();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <class N>
 __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
-  // two weight stages (double buffer) + both hidden biases; A fragments are ds_read_b128 at
+  // a ring of three weight stages + both hidden biases; A fragments are ds_read_b128 at
   // operand*1 KiB + lane*16: conflict-free, and each 1 KiB operand is read by all 4 waves
-  __shared__ __attribute__((aligned(16))) u32x4 stage[2][N::COPS * 64];
-  __shared__ __attribute__((aligned(16))) float bias[N::H0 + N::H1];
+  // ONE __shared__ object: with a second one beside the LDS-DMA target, hipcc (ROCm 7.2) emits
+  // vmcnt(0) before ds_reads and the staging stops overlapping (cdna_hip_programming.md §5, trap (a))
+  __shared__ __attribute__((aligned(16))) u32x4 lds[N::STAGES * N::COPS * 64 + (N::H0 + N::H1) / 4];
+  u32x4 (*stage)[N::COPS * 64] = reinterpret_cast<u32x4 (*)[N::COPS * 64]>(lds);
+  float* bias = reinterpret_cast<float*>(lds + N::STAGES * N::COPS * 64);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (LDS-DMA base in m0)
   const int r = lane & 31, h = lane >> 5;
-  const int64_t s0 = ((int64_t)blockIdx.x * (MT / 64) + w) * 32;
-  const int64_t row = s0 + r;
-  const bool live = row < a.rows;                 // (a wave past the end still joins the barriers)
   const u32x4* chunks = static_cast<const u32x4*>(a.packed);
   const u32x4* W2 = chunks + N::CHUNKS_OPS * 64;
   const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
   const float* b2 = gb + N::H0 + N::H1;
+  // Persistent: one workgroup per CU walks the 128-row tasks, so the weight pipeline (and the
+  // biases) carry over from task to task instead of restarting behind every workgroup's prologue.
+  const int64_t ntask = (a.rows + MT / 2 - 1) / (MT / 2);
+  const int my_tasks = (int)((ntask - blockIdx.x + gridDim.x - 1) / gridDim.x);
 
-  // plain global loads first (biases, observation rows), then the LDS-DMA pipeline
   for (int i = tid; i < N::H0 + N::H1; i += MT) bias[i] = gb[i];
-  bf16x8 xb[N::KQ0];                              // X^T fragments: lane (r,h) holds obs[row][16q+8h+j]
-  const float* x = a.obs + (live ? row : 0) * N::IN;
-#pragma unroll
-  for (int q = 0; q < N::KQ0; ++q) {
-    f32x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 16 * q + 8 * h + j;
-      const float xv = x[k < N::IN ? k : N::IN - 1];        // branch-free: clamp, then select
-      v[j] = (live && k < N::IN) ? xv : 0.0f;
-    }
-    xb[q] = __builtin_convertvector(v, bf16x8);
-  }
-  stage_chunk<N>(chunks, stage[0], w, lane);
+  auto stage_of = [&](int gg) { return stage[gg % N::STAGES]; };
+  // running chunk counter gg = task_iter * NCH + g; chunk gg is weight chunk gg % NCH
+  auto fetch = [&](int gg) {
+    if (gg < my_tasks * N::NCH && !(a.ablate & 1))
+      stage_chunk<N>(chunks + (int64_t)(gg % N::NCH) * N::COPS * 64, stage_of(gg), w, lane);
+  };
+  fetch(0);
   __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): chunk 0 landed
   __syncthreads();
 
-  f32x16 lg{};
-  for (int p = 0; p < N::PASSES; ++p) {
-    f32x16 t1[N::T1P];
+  for (int it = 0; it < my_tasks; ++it) {
+    const int64_t task = blockIdx.x + (int64_t)it * gridDim.x;
+    const int64_t s0 = task * (MT / 2) + w * 32;
+    const int64_t row = s0 + r;
+    const bool live = row < a.rows;               // (a wave past the end still joins the barriers)
+    const int base = it * N::NCH;
+    bf16x8 xb[N::KQ0];                            // X^T fragments: lane (r,h) holds obs[row][16q+8h+j]
+    {
+      const float* x = a.obs + (live ? row : 0) * N::IN;
 #pragma unroll
-    for (int n = 0; n < N::T1P; ++n) t1[n] = f32x16{};
-    for (int c = 0; c < N::NC; ++c) {
-      const int g = p * N::NC + c;                // chunk index
-      if (g + 1 < N::NCH && !(a.ablate & 1))
-        stage_chunk<N>(chunks + (int64_t)(g + 1) * N::COPS * 64, stage[(g + 1) & 1], w, lane);
-      const u32x4* S = stage[g & 1];
-      bf16x8 hb[N::CH][2];
+      for (int q = 0; q < N::KQ0; ++q) {
+        f32x8 v;
 #pragma unroll
-      for (int m = 0; m < N::CH; ++m) {
-        f32x16 t0{};
-#pragma unroll
-        for (int q = 0; q < N::KQ0; ++q) t0 = mfma(frag(S + (m * N::KQ0 + q) * 64 + lane), xb[q], t0);
-        relu_to_frags(t0, bias, 32 * (c * N::CH + m), h, hb[m][0], hb[m][1]);
-      }
-      // layer 1: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and B = hb[m][s].  A
-      // fragments are read from LDS one group of GS ahead of their MFMAs; the sched_barrier keeps
-      // the compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would spill).
-      constexpr int GS = 8, NG = N::CW1 / GS;
-      static_assert(N::CW1 % GS == 0, "layer-1 operand groups");
-      bf16x8 cur[GS], nxt[GS];
-#pragma unroll
-      for (int i = 0; i < GS; ++i) cur[i] = frag(S + (N::CW0 + i) * 64 + lane);
-#pragma unroll
-      for (int gi = 0; gi < NG; ++gi) {
-        if (gi + 1 < NG) {
-#pragma unroll
-          for (int i = 0; i < GS; ++i) nxt[i] = frag(S + (N::CW0 + (gi + 1) * GS + i) * 64 + lane);
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * q + 8 * h + j;
+          const float xv = x[k < N::IN ? k : N::IN - 1];      // branch-free: clamp, then select
+          v[j] = k < N::IN ? (live ? xv : 0.0f) : (k < N::IN + 2 ? 1.0f : 0.0f);   // bias columns
         }
-#pragma unroll
-        for (int i = 0; i < GS; ++i) {
-          const int op = gi * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
-          t1[n] = mfma(cur[i], hb[m][s], t1[n]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < GS; ++i) cur[i] = nxt[i];
+        xb[q] = __builtin_convertvector(v, bf16x8);
       }
-      __builtin_amdgcn_s_waitcnt(0x0F70);         // next chunk landed
-      __syncthreads();                            // ... and nobody still reads the stage it reuses
     }
-    // layer 2 over this pass's hidden tiles
-#pragma unroll
-    for (int nn = 0; nn < N::T1P; ++nn) {
-      const int n = p * N::T1P + nn;
-      bf16x8 f0, f1;
-      relu_to_frags(t1[nn], bias + N::H0, 32 * n, h, f0, f1);
-      lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
-      lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
-      __builtin_amdgcn_sched_barrier(0);          // one tile at a time: no hoisting of all tiles
-    }
-  }
 
-  // logit o of sample r: o 0-3 in lane r regs 0-3, o 4-7 in lane r+32 regs 0-3, o 8 in lane r reg 4
-  float up[4];
+    // Per chunk: layer 0 (bias inside the MFMA) -> ReLU -> layer 1, while chunk g+1 lands.  The
+    // ReLU's dependency bubble in one wave is covered by the other wave on the same SIMD.
+    f32x16 lg{};
+    for (int p = 0; p < N::PASSES; ++p) {
+      const int g0 = base + p * N::NC;
+      f32x16 t1[N::T1P];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) up[e] = __shfl_xor(lg[e], 32);
-  if (h != 0 || !live) return;
-  float z[N::OUT];
+      for (int n = 0; n < N::T1P; ++n) t1[n] = f32x16{};
+      for (int c = 0; c < N::NC; ++c) {
+        const int g = g0 + c;
+        fetch(g + 1);
+        f32x16 t0[N::CH];
+        layer0<N>(stage_of(g), xb, lane, t0);
+        bf16x8 hb[N::CH][2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    z[e] = lg[e] + b2[e];
-    z[4 + e] = up[e] + b2[4 + e];
-  }
-  z[8] = lg[4] + b2[8];
-  if (a.logits) {
+        for (int m = 0; m < N::CH; ++m) relu_to_frags_nb(t0[m], hb[m][0], hb[m][1]);
+        layer1<N>(stage_of(g), hb, lane, t1, [] {});
+        __builtin_amdgcn_s_waitcnt(0x0F70);       // chunk g+1 landed
+        __syncthreads();                          // ... and stage g is free for chunk g+2
+      }
+      // layer 2 over this pass's hidden tiles
 #pragma unroll
-    for (int o = 0; o < N::OUT; ++o) a.logits[row * N::OUT + o] = z[o];
-  }
-  if (!a.actions) return;
-  float best = -INFINITY;
-  int arg = 0;
-  if (a.explore) {
-    // Gumbel-max: argmax(z + g), g = -log(-log u), u in (0,1) from philox(row, step)
-    uint32_t u32[12];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
-                               a.k0, a.k1);
-      u32[4 * b] = v.x;
-      u32[4 * b + 1] = v.y;
-      u32[4 * b + 2] = v.z;
-      u32[4 * b + 3] = v.w;
+      for (int nn = 0; nn < N::T1P; ++nn) {
+        const int n = p * N::T1P + nn;
+        bf16x8 f0, f1;
+        relu_to_frags(t1[nn], bias + N::H0, 32 * n, h, f0, f1);
+        lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
+        lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
+        __builtin_amdgcn_sched_barrier(0);        // one tile at a time: no hoisting of all tiles
+      }
     }
+
+    // logit o of sample r: o 0-3 in lane r regs 0-3, o 4-7 in lane r+32 regs 0-3, o 8 in lane r reg 4
+    float up[4];
 #pragma unroll
-    for (int o = 0; o < N::OUT; ++o) {
-      const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      const float v = z[o] - __logf(-__logf(u));
-      if (v > best) { best = v; arg = o; }
+    for (int e = 0; e < 4; ++e) up[e] = __shfl_xor(lg[e], 32);
+    if (h == 0 && live) {
+      float z[N::OUT];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        z[e] = lg[e] + b2[e];
+        z[4 + e] = up[e] + b2[4 + e];
+      }
+      z[8] = lg[4] + b2[8];
+      if (a.logits) {
+#pragma unroll
+        for (int o = 0; o < N::OUT; ++o) a.logits[row * N::OUT + o] = z[o];
+      }
+      if (a.actions) {
+        float best = -INFINITY;
+        int arg = 0;
+        if (a.explore) {
+          // Gumbel-max: argmax(z + g), g = -log(-log u), u in (0,1) from philox(row, step)
+          uint32_t u32[12];
+#pragma unroll
+          for (int b = 0; b < 3; ++b) {
+            const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
+                                     a.k0, a.k1);
+            u32[4 * b] = v.x;
+            u32[4 * b + 1] = v.y;
+            u32[4 * b + 2] = v.z;
+            u32[4 * b + 3] = v.w;
+          }
+#pragma unroll
+          for (int o = 0; o < N::OUT; ++o) {
+            const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+            const float v = z[o] - __logf(-__logf(u));
+            if (v > best) { best = v; arg = o; }
+          }
+        } else {
+#pragma unroll
+          for (int o = 0; o < N::OUT; ++o)
+            if (z[o] > best) { best = z[o]; arg = o; }   // first maximum wins (numpy/torch argmax)
+        }
+        a.actions[row] = arg;
+      }
     }
-  } else {
-#pragma unroll
-    for (int o = 0; o < N::OUT; ++o)
-      if (z[o] > best) { best = z[o]; arg = o; }   // first maximum wins (numpy/torch argmax)
   }
-  a.actions[row] = arg;
 }
 
 // ------------------------------------------------------------------------------------- host
@@ -254,6 +326,13 @@ uint16_t to_bf16(float f) {   // round to nearest even (NaN not expected in weig
   memcpy(&u, &f, 4);
   u += 0x7FFFu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
+}
+
+float from_bf16(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
 }
 
 template <class N>
@@ -273,8 +352,10 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
       for (int q = 0; q < N::KQ0; ++q)           // W0 [H0][IN], natural k order (X^T from memory)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 8; ++j) {
-            const int k = 16 * q + 8 * (l >> 5) + j;
-            put(base + m * N::KQ0 + q, l, j, k < N::IN ? w0[(int64_t)(32 * t + (l & 31)) * N::IN + k] : 0.0f);
+            const int k = 16 * q + 8 * (l >> 5) + j, o = 32 * t + (l & 31);
+            const float bh = from_bf16(to_bf16(b0[o]));        // b0 = hi + lo, both bf16
+            const float v = k < N::IN ? w0[(int64_t)o * N::IN + k] : k == N::IN ? bh : k == N::IN + 1 ? b0[o] - bh : 0.0f;
+            put(base + m * N::KQ0 + q, l, j, v);
           }
       for (int nn = 0; nn < N::T1P; ++nn)        // W1 [H1][H0], rows of pass p
         for (int s = 0; s < 2; ++s)
@@ -314,9 +395,9 @@ MlpKernel make_mlp() {
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml
   static const MlpKernel reg[] = {
-      make_mlp<37, 256, 256, 4, 1>(),     // Small:  obs 9*4+1,  [256, 256]
-      make_mlp<82, 512, 512, 2, 2>(),     // Medium: obs 9*9+1,  [512, 512]
-      make_mlp<145, 1024, 256, 2, 1>(),   // Large:  obs 9*16+1, [1024, 256]
+      make_mlp<37, 256, 256, 4, 2>(),     // Small:  obs 9*4+1,  [256, 256]
+      make_mlp<82, 512, 512, 4, 4>(),     // Medium: obs 9*9+1,  [512, 512]
+      make_mlp<145, 1024, 256, 2, 2>(),   // Large:  obs 9*16+1, [1024, 256]
   };
   if (!d || d->out_dim != 9) return nullptr;
   for (const auto& k : reg)
@@ -357,9 +438,16 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
   const char* abl = getenv("WH_MLP_ABLATE");
   MlpArgs a{packed, rows, obs, logits, actions, explore ? 1 : 0, (uint32_t)(seed & 0xFFFFFFFFu),
             (uint32_t)(seed >> 32), step, abl ? atoi(abl) : 0};
-  const int64_t rows_per_wg = 32 * (MT / 64);
-  hipLaunchKernelGGL(k->fwd, dim3((unsigned)((rows + rows_per_wg - 1) / rows_per_wg)), dim3(MT), 0,
-                     (hipStream_t)stream, a);
+  static int cus = 0;                         // one persistent workgroup per CU
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return WH_EHIP;
+    cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  }
+  const int64_t ntask = (rows + MT / 2 - 1) / (MT / 2);
+  const unsigned grid = (unsigned)(ntask < cus ? ntask : cus);
+  hipLaunchKernelGGL(k->fwd, dim3(grid), dim3(MT), 0, (hipStream_t)stream, a);
   return hip_rc(hipGetLastError());
 }
 
