@@ -1,6 +1,10 @@
+# Round-1 evidence: the default bench line, then rocprofv3 kernel-trace/stats + FETCH/WRITE passes
+# for each measured kernel (fused step with SQ counters, 1-step graph, observation rows, policy
+# MLP).  Summaries go to profiles/ via tools/pmc_summary.py (run here afterwards).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 && \
-SQ=1 bash tools/profile_round.sh medium_n8_fused --no-alt --no-sampler && \
-bash tools/profile_round.sh medium_n8_graph --mode graph --no-alt --no-sampler && \
-bash tools/profile_round.sh medium_n8_observe --no-alt
+SQ=1 bash tools/profile_round.sh medium_n8_fused --no-alt --no-sampler --no-policy && \
+bash tools/profile_round.sh medium_n8_graph --mode graph --no-alt --no-sampler --no-policy && \
+bash tools/profile_round.sh medium_n8_observe --no-alt --no-policy && \
+bash tools/profile_round.sh medium_n8_mlp --no-alt --no-sampler --steps 400 --policy-steps 60
