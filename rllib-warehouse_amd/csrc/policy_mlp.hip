@@ -13,11 +13,16 @@
 //    ReLU + v_cvt_pk_bf16_f32, registers 8s..8s+7 ARE the B operand of k-step s of the next layer
 //    (cdna_hip_programming.md §3, "accumulator tile as the next MFMA's operand"): activations
 //    never leave registers.  The permuted k order this implies is folded into the packed weights.
-//  * Layer 0 is streamed in chunks of CH hidden tiles straight into layer 1's accumulators, so
-//    only layer 1's [H1 x 32] accumulators (+ one chunk) are live: <= 512 registers per lane at
-//    one wave per SIMD for all three variants.
-//  * Weights are packed once (wh_mlp_pack) in fragment order: one MFMA A operand = 64 lanes x 16
-//    contiguous bytes, one dwordx4 load per lane.
+//  * Layer 0 is streamed in chunks of CH hidden tiles straight into layer 1's accumulators, and
+//    layer-1 rows are produced in PASSES passes, so only T1P x 16 accumulator registers (+ one
+//    chunk) are live: <= 256 registers per lane, two waves per SIMD (8 per workgroup).
+//  * Layer 0's bias rides in the MFMA (two input columns fixed at 1.0 carry b0 as bf16 hi + lo);
+//    ReLU runs on the packed bf16 bits (v_pk_max_i16 with 0).
+//  * Weights are packed once (wh_mlp_pack) in fragment order, one MFMA A operand = 64 lanes x 16
+//    contiguous bytes, and streamed chunk by chunk into two LDS stages by LDS-DMA
+//    (global_load_lds_dwordx4, lane-linear); all 8 waves read every staged operand.
+//  * Persistent workgroups (one per CU) walk 256-row tasks, so the weight pipeline and the
+//    biases carry over from task to task.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -127,7 +132,7 @@ __device__ __forceinline__ void relu_to_frags_nb(f32x16 t, bf16x8& f0, bf16x8& f
 }
 
 // One chunk of packed weights (COPS operands) global -> LDS stage by LDS-DMA: each wave copies
-// every 4th operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
+// every (MT/64)-th operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
 template <class N>
 __device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4* dst, int w, int lane) {
 #pragma unroll
@@ -155,13 +160,12 @@ __device__ __forceinline__ void layer0(const u32x4* S, const bf16x8 (&xb)[N::KQ0
 }
 
 // Layer-1 MFMAs of one chunk: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and
-// B = hb[m][s].  A fragments are read from LDS one group of GS ahead of their MFMAs; the
-// sched_barrier keeps the compiler from hoisting all CW1 reads at once (CW1 x 4 VGPRs would
-// spill).  `mid` runs once, between two MFMA groups half-way through (the next chunk's ReLU goes
-// there, so its VALU work issues under this chunk's MFMAs).
-template <class N, class Mid>
+// B = hb[m][s].  A fragments are read from LDS DEPTH groups of GS ahead of their MFMAs; the
+// sched_barriers keep the reads ahead of the MFMAs and stop the compiler from hoisting all CW1
+// reads at once (CW1 x 4 VGPRs would spill).
+template <class N>
 __device__ __forceinline__ void layer1(const u32x4* S, const bf16x8 (&hb)[N::CH][2], int lane,
-                                       f32x16 (&t1)[N::T1P], Mid mid) {
+                                       f32x16 (&t1)[N::T1P]) {
   constexpr int GS = 4, NG = N::CW1 / GS, DEPTH = 2;   // fragments read DEPTH groups ahead
   static_assert(N::CW1 % GS == 0 && NG >= DEPTH, "layer-1 operand groups");
   bf16x8 buf[DEPTH + 1][GS];
@@ -181,15 +185,14 @@ __device__ __forceinline__ void layer1(const u32x4* S, const bf16x8 (&hb)[N::CH]
       const int op = gi * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
       t1[n] = mfma(buf[gi % (DEPTH + 1)][i], hb[m][s], t1[n]);
     }
-    if (gi == NG / 2) mid();
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 template <class N>
 __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
-  // a ring of three weight stages + both hidden biases; A fragments are ds_read_b128 at
-  // operand*1 KiB + lane*16: conflict-free, and each 1 KiB operand is read by all 4 waves
+  // two weight stages + both hidden biases; A fragments are ds_read_b128 at operand*1 KiB +
+  // lane*16: conflict-free, and each 1 KiB operand is read by all 8 waves.
   // ONE __shared__ object: with a second one beside the LDS-DMA target, hipcc (ROCm 7.2) emits
   // vmcnt(0) before ds_reads and the staging stops overlapping (cdna_hip_programming.md §5, trap (a))
   __shared__ __attribute__((aligned(16))) u32x4 lds[N::STAGES * N::COPS * 64 + (N::H0 + N::H1) / 4];
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
   const u32x4* W2 = chunks + N::CHUNKS_OPS * 64;
   const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
   const float* b2 = gb + N::H0 + N::H1;
-  // Persistent: one workgroup per CU walks the 128-row tasks, so the weight pipeline (and the
+  // Persistent: one workgroup per CU walks the 256-row tasks, so the weight pipeline (and the
   // biases) carry over from task to task instead of restarting behind every workgroup's prologue.
   const int64_t ntask = (a.rows + MT / 2 - 1) / (MT / 2);
   const int my_tasks = (int)((ntask - blockIdx.x + gridDim.x - 1) / gridDim.x);
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
         bf16x8 hb[N::CH][2];
 #pragma unroll
         for (int m = 0; m < N::CH; ++m) relu_to_frags_nb(t0[m], hb[m][0], hb[m][1]);
-        layer1<N>(stage_of(g), hb, lane, t1, [] {});
+        layer1<N>(stage_of(g), hb, lane, t1);
         __builtin_amdgcn_s_waitcnt(0x0F70);       // chunk g+1 landed
         __syncthreads();                          // ... and stage g is free for chunk g+2
       }
