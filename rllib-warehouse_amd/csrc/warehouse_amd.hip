@@ -439,8 +439,14 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329)
     bool looked = false;
     if (!(ablate & 2)) {
+      // The grid is rebuilt as {live agents' cells} (core.py:275-276) by OR-ing the cells into
+      // what the previous step left, which is always a subset of them (a set bit is an arrival
+      // or an agent that stayed; leaving clears), so no per-step clear is needed.  k_step clears
+      // it at launch and after an auto-reset; the ordered (drop-in) path clears it every step.
+      if (ORDERED) {
 #pragma unroll
-      for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+      }
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         const uint32_t p = s.ag[i] & XY16;
@@ -744,6 +750,8 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
+#pragma unroll
+  for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
 
   if (a.phase == PH_POLICY) {
     uint32_t d[C::NAM];
@@ -792,7 +800,11 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
         if (__any(done)) flush_episodes(done, (s.hdr >> 16) & 0xFFu, epr, a.stats);
         if (done) epr = 0;
       }
-      if (done && a.autoreset && !(a.ablate & 128)) reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
+      if (done && a.autoreset && !(a.ablate & 128)) {
+        reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
+#pragma unroll
+        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+      }
     }
   }
   if (a.returns) a.returns[e] += ret;

@@ -13,6 +13,8 @@ from typing import Optional
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libwarehouse_amd.so")
+# kernel A/B experiments (tools/ab.sh) point this at an alternative build of the same library
+LIB_PATH = os.environ.get("WAREHOUSE_AMD_LIB", LIB_PATH)
 
 WH_OK = 0
 WH_EINVAL = 22
