@@ -16,6 +16,7 @@ For thousands of envs use `warehouse.batched.BatchedWarehouse` (device philox dr
 from __future__ import annotations
 
 import os
+import time
 from typing import Dict, List, Tuple
 
 import numpy as np
@@ -40,7 +41,7 @@ def _default_device():
 
 
 class Warehouse(MultiAgentEnv):
-    metadata = {"render.modes": ["human"]}
+    metadata = {"render.modes": ["human", "ansi", "rgb_array"]}
 
     def __init__(self, num_agents: int, num_requests: int, area_dimension: int,
                  pickup_racks_arrangement: List[int], episode_duration: int,
@@ -85,6 +86,8 @@ class Warehouse(MultiAgentEnv):
         w = {k: n for k, n in zip(OBS_KEYS, (1, R - 1, 2 * (R - 1), 2 * (R - 1), 4 * R, 1, 2, 2))}
         self._obs_split = np.cumsum([w[k] for k in OBS_KEYS])[:-1]
         self._done = False
+        self._prev = None          # host snapshot before the last step (core.py:270-272), kept
+        self._rendering = False    # only once render() has been called: it costs a device copy
 
     # ------------------------------------------------------------------ helpers
     def _obs_dicts(self) -> Dict[str, Dict[str, np.ndarray]]:
@@ -136,6 +139,8 @@ class Warehouse(MultiAgentEnv):
             order[0, s] = idx
             acts[0, idx] = a % 9                             # Python's negative-index wrap
         eng = self._engine
+        if self._rendering:
+            self._prev = self._snapshot()                    # core.py:270-272
         eng.step(acts, order=order, phase=nat.WH_PHASE_PRE_REGEN)
         n_in = int(eng.n_inactive[0].item())
         k = R - self._num_pickup_points + n_in
@@ -153,5 +158,64 @@ class Warehouse(MultiAgentEnv):
         dones["__all__"] = done
         return obs, rewards, dones, {str(i): {} for i in range(n)}
 
-    def render(self, mode: str = "human", animate: bool = False) -> None:
-        raise NotImplementedError("rendering (core.py:444-617) is out of scope for the GPU build")
+    # ------------------------------------------------------------------ rendering
+    def _snapshot(self) -> Dict[str, np.ndarray]:
+        c = self._engine.to_canonical()
+        return dict(pos=c["pos"][0].cpu().numpy(), agent_target=c["agent_target"][0].cpu().numpy(),
+                    pickup_target=c["pickup_target"][0].cpu().numpy())
+
+    def _frame_text(self, snap: Dict[str, np.ndarray]) -> str:
+        """One frame as text, row y = D-1 at the top (the reference's viewer has y up):
+        '.' floor, '#' pickup point, 'P' pickup point with an open request, 'D' delivery point,
+        agents 'a', 'b', ... when idle and 'A', 'B', ... when carrying, '*' for a shared cell."""
+        D = self._area_dimension
+        grid = [["." for _ in range(D)] for _ in range(D)]
+        pk = pickup_cells(D, self._pickup_racks_arrangement)
+        for j, (x, y) in enumerate(pk):
+            grid[y][x] = "P" if snap["pickup_target"][j] >= 0 else "#"
+        for v in range(2, D - 2):                             # core.py:177-188
+            for x, y in ((v, 0), (0, v), (v, D - 1), (D - 1, v)):
+                grid[y][x] = "D"
+        for i, (x, y) in enumerate(snap["pos"]):
+            ch = chr((ord("A") if snap["agent_target"][i] >= 0 else ord("a")) + i % 26)
+            grid[y][x] = "*" if grid[y][x] not in ".#PD" else ch
+        return "\n".join("".join(row) for row in reversed(grid))
+
+    def _frame_rgb(self, pos: np.ndarray, snap: Dict[str, np.ndarray], px: int = 12) -> np.ndarray:
+        D = self._area_dimension
+        img = np.full((D * px, D * px, 3), 235, np.uint8)
+        def fill(x, y, c, m=0):
+            img[(D - 1 - y) * px + m:(D - y) * px - m, x * px + m:(x + 1) * px - m] = c
+        for j, (x, y) in enumerate(pickup_cells(D, self._pickup_racks_arrangement)):
+            fill(x, y, (230, 160, 40) if snap["pickup_target"][j] >= 0 else (170, 170, 170))
+        for v in range(2, D - 2):
+            for x, y in ((v, 0), (0, v), (v, D - 1), (D - 1, v)):
+                fill(x, y, (90, 160, 230))
+        for i, (x, y) in enumerate(np.rint(pos).astype(int)):
+            fill(int(x), int(y), (200, 40, 40) if snap["agent_target"][i] >= 0 else (40, 150, 60), m=2)
+        return img
+
+    def render(self, mode: str = "human", animate: bool = False):
+        """Headless rendering of the device state (the reference draws the same scene with a gym
+        pyglet Viewer, core.py:444-617).  mode "human" prints the frame, "ansi" returns it as
+        text, "rgb_array" returns an RGB image -- with animate=True a list of
+        animate_frames_per_step images moving the agents from their previous cells
+        (core.py:449-469); "human" then keeps the reference's pacing of
+        animate_steps_per_second."""
+        if mode not in self.metadata["render.modes"]:
+            raise NotImplementedError(f"render mode {mode!r}")
+        self._rendering = True
+        snap = self._snapshot()
+        prev = self._prev if self._prev is not None else snap
+        if mode == "rgb_array":
+            if not animate:
+                return self._frame_rgb(snap["pos"], snap)
+            f = self.animate_frames_per_step
+            return [self._frame_rgb(prev["pos"] + (snap["pos"] - prev["pos"]) / f * i, prev) for i in range(f)]
+        text = self._frame_text(snap)
+        if mode == "ansi":
+            return text
+        print(text, flush=True)
+        if animate:
+            time.sleep(1.0 / self.animate_steps_per_second)
+        return None

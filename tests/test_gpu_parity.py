@@ -360,3 +360,31 @@ def test_c5_eight_shards_equal_one_batch_of_524288(wh):
     assert ((c["pickup_timer"] >= 0) == active).all()
     assert c["pos"].min() >= 0 and c["pos"].max() < L.D
     assert float(rew.sum()) > 0
+
+
+def test_dropin_render_headless(wh):
+    """Rendering (core.py:444-617) from a host copy of the device state: the text
+    frame puts every agent on its cell and every open request on its pickup point; animate=True
+    yields animate_frames_per_step RGB frames from the previous cells (core.py:270-272, 449-469)."""
+    np.random.seed(3)
+    env = wh.WarehouseSmall(2)
+    env.reset()
+    D = 12
+    txt = env.render(mode="ansi")
+    rows = txt.split("\n")
+    assert len(rows) == D and all(len(r) == D for r in rows)
+    snap = env._snapshot()
+    for i, (x, y) in enumerate(snap["pos"]):
+        assert rows[D - 1 - y][x] in (chr(ord("a") + i), "*")
+    covered = {tuple(p) for p in snap["pos"]}
+    from warehouse._geometry import pickup_cells
+
+    open_cells = [c for j, c in enumerate(pickup_cells(D, (4, 8))) if snap["pickup_target"][j] >= 0]
+    assert len(open_cells) == 4
+    assert txt.count("P") == sum(1 for c in open_cells if c not in covered)
+    env.step({"0": 4, "1": 5})
+    frames = env.render(mode="rgb_array", animate=True)
+    assert len(frames) == env.animate_frames_per_step and frames[0].shape == (D * 12, D * 12, 3)
+    assert env.render(mode="rgb_array").dtype == np.uint8
+    with pytest.raises(NotImplementedError):
+        env.render(mode="bogus")
