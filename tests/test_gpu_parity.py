@@ -388,3 +388,33 @@ def test_dropin_render_headless(wh):
     assert env.render(mode="rgb_array").dtype == np.uint8
     with pytest.raises(NotImplementedError):
         env.render(mode="bogus")
+
+
+def test_max_size_batch_2m_envs(wh):
+    """2,097,152 Medium x 8 envs on one GPU (32x the per-GPU C3 batch): 64-bit offsets in the
+    step, reward, observation and policy paths.  A sampled subset of env ids (including the last
+    ones) equals the oracle after a fused greedy rollout, and the observation rows match."""
+    import torch
+
+    B, seed, K = 1 << 21, 21, 6
+    L = oc.layout_for("medium")
+    env = wh.BatchedWarehouse("medium", B, 8, seed=seed)
+    env.reset()
+    rew = torch.zeros((K, B, 8), device=env.device)
+    env.rollout(K, "greedy", 0.0, rewards=rew)
+    ids = np.concatenate([np.random.RandomState(2).choice(B - 64, 192, replace=False), np.arange(B - 64, B)])
+    S = ob.BState.zeros(L, len(ids), 8)
+    d = ob.PhiloxDraws(seed, ids)
+    ob.reset(L, S, d)
+    orew = []
+    for _ in range(K):
+        r, _, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        orew.append(r)
+    c = canon(env)
+    assert_same({k: v[ids] for k, v in c.items()}, S, "subset")
+    np.testing.assert_array_equal(rew[:, torch.as_tensor(ids, device=env.device)].cpu().numpy(), np.stack(orew))
+    obs = env.observe()
+    np.testing.assert_array_equal(obs[torch.as_tensor(ids, device=env.device)].cpu().numpy(), ob.observe(L, S))
+    acts = env.policy("greedy", 0.0)
+    np.testing.assert_array_equal(acts[torch.as_tensor(ids, device=env.device)].cpu().numpy(),
+                                  ob.greedy(L, S, 0.0, d))
