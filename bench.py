@@ -93,6 +93,13 @@ def load_traffic(tag):
         return None
 
 
+def config_name(variant, na, envs, policy):
+    """BASELINE.json config this run corresponds to (SURVEY §8 notation), else 'custom'."""
+    known = {("small", 4, 4096, "random"): "C2", ("medium", 8, 65536, "greedy"): "C3",
+             ("large", 16, 65536, "greedy"): "C4"}
+    return known.get((variant, na, envs, policy), "custom")
+
+
 def load_issue(tag, steps_per_launch):
     """VALU issue view of the step kernel from the committed SQ counters (tools/profile_round.sh
     with SQ=1 -> profiles/pmc_traffic.json): per wave and env-step, VALU instructions and wave
@@ -389,8 +396,8 @@ def main():
             "dtype": "u8/u32 packed integer state, f32 rewards",
             "data": "synthetic: philox-seeded episodes keyed by global env id, greedy policy on device",
             "config": {
-                "workload": f"C3: {args.variant} N={NA}, B={B} envs/GPU, {args.policy} policy fused with "
-                            f"step + auto-reset (device-resident rollout)",
+                "workload": f"{config_name(args.variant, NA, B, args.policy)}: {args.variant} N={NA}, B={B} envs/GPU, "
+                            f"{args.policy} policy fused with step + auto-reset (device-resident rollout)",
                 "envs_per_gpu": B, "agents": NA, "variant": args.variant, "policy": args.policy,
                 "launch": "hipGraph of 1-step launches" if args.mode == "graph" else f"{spl} steps per launch",
                 "parallelism": f"independent env shards x{world}, no collectives",
