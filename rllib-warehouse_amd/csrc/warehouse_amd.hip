@@ -45,8 +45,9 @@ constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 struct TableLayout {
   int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
-      : cell(0), rp(32 * D), tag(32 * D + 4 * P), dst(32 * D + 8 * P), mv(32 * D + 8 * P + 4 * DP),
-        valid(32 * D + 8 * P + 4 * DP + 48), bytes(32 * D + 8 * P + 4 * DP + 48 + 4 * NV) {}
+      : cell(0), rp(32 * D), tag(32 * D + 4 * (P + 1)), dst(32 * D + 8 * (P + 1)),
+        mv(32 * D + 8 * (P + 1) + 4 * DP), valid(32 * D + 8 * (P + 1) + 4 * DP + 48),
+        bytes(32 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
 
 template <int D_, int R_, int NR_, int NAM_>
@@ -129,6 +130,18 @@ __device__ __forceinline__ uint32_t expand_nib(uint32_t nib) {
   const uint32_t ones = __umul24(nib, 0x00204081u) & 0x01010101u;
   return (ones << 8) - ones;
 }
+
+// Branch-free selects without VCC: a one-wave-per-SIMD kernel pays for every v_cmp -> SGPR mask ->
+// v_cndmask round trip (measured: tools/oprate3.hip), while v_bitop3 is a plain full-rate VALU op.
+// Masks are 0 / 0xFFFFFFFF in VGPRs; every consumer goes through the bitop3 builtin so LLVM cannot
+// fold the mask arithmetic back into compare + select.
+constexpr uint32_t TA = 0xF0, TB = 0xCC, TC = 0xAA;   // truth-table columns of operands 0, 1, 2
+template <uint32_t TT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)(TT & 0xFFu));
+}
+__device__ __forceinline__ uint32_t mask_z(uint32_t x) { return (uint32_t)((int32_t)(x - 1u) >> 31); }   // x == 0 (x < 2^31)
+__device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { return bop3<(TA & TB) | (~TA & TC)>(m, a, b); }
 
 // packed i16 max/min, pinned: hipcc rewrites clamp(x, -1, 1) on i16 pairs into per-half
 // compare/select cascades (it recognises sign(x)); one v_pk_* op per bound is what we want.
@@ -324,12 +337,11 @@ __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e,
 // availability 0 (fresh reset, or carrying) -> head for the own delivery target (the null cell
 // after reset), else for the nearest open request by Manhattan distance, first (lowest pickup
 // index) minimum wins; step = clip(goal - pos, -1, 1).  Random actions come from the
-// POLICY/RANDOM streams.  Slots >= n stay (d = 0).
+// POLICY/RANDOM streams.  Slots >= n get arbitrary steps: step_env never moves them.
 template <class C, int POLICY>
 __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, const Keys& k,
                                              uint32_t gid, float p, uint32_t (&d)[C::NAM]) {
   const uint32_t t = s.hdr & 0xFFFFu;
-  const uint32_t n = (s.hdr >> 16) & 0xFFu;
   if (POLICY == POL_RANDOM) {
 #pragma unroll
     for (int b = 0; b < (C::NAM + 3) / 4; ++b) {
@@ -342,21 +354,29 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
     }
   } else {
     asm volatile("; PHASE policy_rtag" ::: "memory");
-    const bool fresh = (s.hdr >> 24) & 1u;
-    // open requests in ascending pickup order (core.py:409-418)
+    // Open requests in ascending pickup order (core.py:409-418).  Index P of the tables is a
+    // sentinel (far-away cell, null-cell tag) that fills missing slots; after a reset every slot is
+    // the sentinel, so every agent's "nearest request" is the null cell, which is where the
+    // reference's reset observation sends the greedy solver (availability 0, core.py:233-236).
+    const uint32_t mf = 0u - ((s.hdr >> 24) & 1u);
+    uint32_t mlo = bop3<~TA & TB>(mf, (uint32_t)s.am, 0u);
+    uint32_t mhi = bop3<~TA & TB>(mf, (uint32_t)(s.am >> 32), 0u);
     uint32_t rp[C::R], tg[C::R];
-    uint64_t m = s.am;
 #pragma unroll
     for (int r = 0; r < C::R; ++r) {
-      const bool has = m != 0ull;
-      const uint32_t j = has ? (uint32_t)__builtin_ctzll(m) : 0u;
-      const uint32_t a = L.rp(j), b = L.tag(j);
-      rp[r] = has ? a : XY16;           // a far-away cell: never the minimum
-      tg[r] = has ? b : 0xFFFFu;
+      uint32_t flo, fhi;
+      asm("v_ffbl_b32 %0, %1" : "=v"(flo) : "v"(mlo));   // 0xFFFFFFFF when empty
+      asm("v_ffbl_b32 %0, %1" : "=v"(fhi) : "v"(mhi));
+      const uint32_t j = __builtin_elementwise_min(
+          __builtin_elementwise_min(flo, __builtin_elementwise_add_sat(fhi, 32u)), (uint32_t)C::P);
+      rp[r] = L.rp(j);
+      tg[r] = L.tag(j);
+      uint64_t m = ((uint64_t)mhi << 32) | mlo;
       m &= m - 1ull;
+      mlo = (uint32_t)m;
+      mhi = (uint32_t)(m >> 32);
     }
     asm volatile("; PHASE policy_agents" ::: "memory");
-    constexpr uint32_t null16 = (uint32_t)(C::D / 2) | ((uint32_t)(C::D / 2) << 16);
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i) {
       const uint32_t a = s.ag[i];
@@ -367,9 +387,8 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
         best = min(best, __builtin_amdgcn_sad_hi_u8(pos, rp[r], tg[r]));
       const uint32_t near = ((best >> 5) & 31u) | ((best & 31u) << 16);
       const uint32_t dst = (a >> 8) & XY16;
-      const bool carrying = (a & 0xFF00u) != 0xFF00u;
-      uint32_t goal = carrying ? dst : near;
-      goal = fresh ? null16 : goal;
+      const uint32_t idle = (uint32_t)__builtin_amdgcn_sbfe((int)a, 15, 1);   // target byte 0xFF
+      const uint32_t goal = msel(idle, near, dst);
       d[i] = pk_min_i16(pk_max_i16(pk_sub_i16(goal, pos), 0xFFFFFFFFu), 0x00010001u);
     }
     if (p > 0.0f) {
@@ -388,8 +407,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < C::NAM; ++i) d[i] = (i < (int)n) ? d[i] : 0u;
+  // (slots >= n: whatever d says, step_env never moves them)
 }
 
 // ----------------------------------------------------------------------------- step
@@ -406,11 +424,12 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
                                          int tid, int ablate) {
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   uint32_t t = s.hdr & 0xFFFFu;
+  uint32_t rewm[C::NAM];   // reward masks: all-ones = 1.0f
 
   if (phase != PH_REGEN) {
     t = (t + 1u) & 0xFFFFu;                                 // core.py:267
 #pragma unroll
-    for (int i = 0; i < C::NAM; ++i) rew[i] = 0.0f;
+    for (int i = 0; i < C::NAM; ++i) rewm[i] = 0u;
 
     // ---- request expiry (core.py:303-306), 4 pickup points per op.  Run before the move: expiry
     //      reads no positions and the move reads no requests, so the two commute, and the pickup
@@ -550,11 +569,15 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       uint64_t picked = 0;
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
+        // take iff on a pickup point (cp != 0) with an open request (tb != 0) and idle: slots >= n
+        // sit idle on the corner cell (0, 0), which is no pickup point.  min3 of the three 0/1-ish
+        // terms is 1 exactly when all hold.
         const uint32_t a = s.ag[i];
-        const bool take = (i < (int)n) & (cp[i] != 0u) & ((a & 0xFF00u) == 0xFF00u) & (tb[i] != 0u);
-        s.ag[i] = take ? ((a & XY16) | (dst[i] << 8)) : a;
-        picked |= take ? (1ull << ((cp[i] - 1u) & 63u)) : 0ull;
-        rew[i] = take ? 1.0f : 0.0f;
+        const uint32_t idle01 = ((a & 0xFF00u) + 0x100u) >> 16;
+        const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cp[i], tb[i]), idle01);
+        s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dst[i] << 8, IDLE);   // idle target bytes are 0xFF
+        picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cp[i] - 1u) & 63u);
+        rewm[i] = m;
       }
 #pragma unroll
       for (int w = 0; w < C::PW; ++w) {
@@ -626,11 +649,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         const uint32_t a = s.ag[i];
-        const bool arrived = ((a >> 8) & XY16) == (a & XY16);
-        s.ag[i] = arrived ? (a | IDLE) : a;
-        rew[i] += arrived ? 1.0f : 0.0f;
+        const uint32_t m = mask_z(bop3<(TA ^ TB) & TC>(a >> 8, a, XY16));   // target cell == position
+        s.ag[i] = bop3<(TA & TB) | TC>(m, IDLE, a);
+        rewm[i] |= m;   // a pickup (interior cell) and a delivery (border cell) never share a step
       }
     }
+#pragma unroll
+    for (int i = 0; i < C::NAM; ++i) rew[i] = __uint_as_float(bop3<TA & TB>(rewm[i], 0x3F800000u, 0u));
     asm volatile("; PHASE tail" ::: "memory");
     done = t >= T;                                            // core.py:438
     s.hdr = t | (n << 16);                                    // clears `fresh`
@@ -1131,8 +1156,9 @@ int validate(const wh_config* c, Geometry* g) {
 
 // Host copy of the per-workgroup tables, same layout as TableLayout (core.py:170-199):
 //   cell  [32*D] u8  : (x | y << 5) -> pickup index + 1, 0 = not a pickup cell
-//   rp    [P]    u32 : pickup cell as x | y << 16
-//   tag   [P]    u32 : pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58)
+//   rp    [P+1]  u32 : pickup cell as x | y << 16; [P] = far-away cell (never nearest)
+//   tag   [P+1]  u32 : pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58);
+//                      [P] = the null cell (D/2, D/2): where fresh-reset agents head (core.py:233-236)
 //   dst   [Dp]   u32 : delivery cell as x | y << 16
 //   mv    [12]   u32 : MOVES[a] as packed i16 (dx, dy) (core.py:38)
 //   valid [NV]   u32 : interior non-pickup cells x | y << 16, ascending (x, y) (spawn, core.py:191-199)
@@ -1141,7 +1167,9 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   *bad = 0;
   if (D > 32) { *bad = 1; return {}; }
   std::vector<uint8_t> cell(32 * D, 0);
-  std::vector<uint32_t> rp(g.P), tag(g.P);
+  std::vector<uint32_t> rp(g.P + 1), tag(g.P + 1);
+  rp[g.P] = 0x00FF00FFu;
+  tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);
   for (int ix = 0; ix < g.NR; ++ix)
     for (int iy = 0; iy < g.NR; ++iy)
       for (int q = 0; q < 4; ++q) {
