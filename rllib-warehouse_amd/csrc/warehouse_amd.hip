@@ -469,7 +469,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         const uint32_t p = s.ag[i] & XY16;
-        atomicOr(&L.occ[p >> 16][tid], (i < (int)n) ? (1u << (p & 31u)) : 0u);
+        const uint32_t mlive = (uint32_t)((int32_t)((uint32_t)i - n) >> 31);
+        atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
       }
       // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
       uint32_t kk[3 * C::NAM];
@@ -515,39 +516,46 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           pp[i] = s.ag[i] & XY16;
           cc[i] = step16<C::D>(pp[i], dstep[i]);
         }
+        // Predicates are kept in bit 31 of VGPRs (x31 names) and selects are v_bitop3 with
+        // 0 / all-ones masks (m names): no VCC round trips on the serial chain.
         uint32_t raw = L.occ[cc[0] >> 16][tid];
-        bool okp = false;
+        uint32_t mokp = 0u;
 #pragma unroll
         for (int sidx = 0; sidx < C::NAM; ++sidx) {
           const uint32_t p = pp[sidx], c = cc[sidx], a = s.ag[sidx];
-          bool occupied = (raw >> (c & 31u)) & 1u;
-          if (sidx > 0) {   // agent sidx-1 cleared its old cell, then set its new one
-            const bool set = okp && c == cc[sidx - 1];
-            const bool clr = okp && c == pp[sidx - 1];
-            occupied = set || (occupied && !clr);
+          // occupied: bit c of the row word, corrected for agent sidx-1's clear-then-set
+          uint32_t occ31 = (uint32_t)__builtin_amdgcn_sbfe((int)raw, c, 1);
+          if (sidx > 0) {
+            const uint32_t set31 = (c ^ cc[sidx - 1]) - 1u;   // bit 31: c == its new cell
+            const uint32_t clr31 = (c ^ pp[sidx - 1]) - 1u;   // bit 31: c == its old cell
+            occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokp, set31, bop3<TC & ~(TA & TB)>(mokp, clr31, occ31));
           }
           if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
           const uint32_t key = p | (c << 8);
-          uint32_t f = 0xFFFFFFFFu;
+          uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
 #pragma unroll
           for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
-          const bool ok = (sidx < (int)n) && !occupied && f != 0u;
-          atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
-          atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
-          const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u), c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);
+          const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
+          const uint32_t mok = (uint32_t)((int32_t)bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u) >> 31);
+          atomicAnd(&L.occ[p >> 16][tid], bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
+          atomicOr(&L.occ[c >> 16][tid], bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
           const uint32_t dxy = c ^ p;
-          const bool diag = ok && (dxy & 0xFFFFu) && (dxy >> 16);
-          kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
-          kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
-          kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
-          const uint32_t moved = ok ? ((a & ~XY16) | c) : a;
+          // diagonal: both 16-bit halves of dxy nonzero (bit 15 of each half after + 0x7FFF)
+          const uint32_t nzh = dxy + 0x7FFF7FFFu;
+          const uint32_t mdiag = (uint32_t)((int32_t)bop3<TA & TB & TC>(nzh, nzh << 16, mok) >> 31);
+          const uint32_t c1 = bop3<(TA & TC) | (TB & ~TC)>(c, p, 0xFFFFu);   // (cx, py)
+          const uint32_t c2 = bop3<(TA & TC) | (TB & ~TC)>(p, c, 0xFFFFu);   // (px, cy)
+          kk[3 * sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
+          kk[3 * sidx + 1] = bop3<~TA | TB>(mdiag, c1 | (c2 << 8), 0u);
+          kk[3 * sidx + 2] = bop3<~TA | TB>(mdiag, c2 | (c1 << 8), 0u);
+          const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
           s.ag[sidx] = moved;
-          okp = ok;
+          mokp = mok;
           cp[sidx] = L.cell_pickup(moved & XY16);
-          if (sidx >= 1) tb[sidx - 1] = *L.ptl_byte(cp[sidx - 1] ? cp[sidx - 1] - 1u : 0u, tid);
+          if (sidx >= 1) tb[sidx - 1] = *L.ptl_byte(min(cp[sidx - 1] - 1u, (uint32_t)(4 * C::PW)), tid);
           if (sidx >= 2) dst[sidx - 2] = L.dst((tb[sidx - 2] - 1u) & 63u);
         }
-        tb[C::NAM - 1] = *L.ptl_byte(cp[C::NAM - 1] ? cp[C::NAM - 1] - 1u : 0u, tid);
+        tb[C::NAM - 1] = *L.ptl_byte(min(cp[C::NAM - 1] - 1u, (uint32_t)(4 * C::PW)), tid);
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst((tb[C::NAM - 2] - 1u) & 63u);
         dst[C::NAM - 1] = L.dst((tb[C::NAM - 1] - 1u) & 63u);
         looked = true;
@@ -562,7 +570,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
 #pragma unroll
-        for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(cp[i] ? cp[i] - 1u : 0u, tid);
+        for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(min(cp[i] - 1u, (uint32_t)(4 * C::PW)), tid);
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
       }
