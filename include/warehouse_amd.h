@@ -20,8 +20,10 @@
  *                      carries nothing; slots >= n hold 0xFF00FF00 (idle at (0,0))
  *     next P/4 words   pickup point j, byte j%4 of word j/4: (request target + 1, 0 = no request)
  *                      (core.py:158)
- *     next P/4 words   pickup point j: remaining wait (core.py:159; 0 when no request)
- *   NA = cfg.agent_slots, P = 4 * num_racks^2.  Slots >= n are all-zero.
+ *     next P/4 words   pickup point j: low 8 bits of the step at which its request expires
+ *                      (opened at step t0: t0 + W; steps left = (byte - t) mod 256, core.py:159;
+ *                      don't-care when the point has no request)
+ *   NA = cfg.agent_slots, P = 4 * num_racks^2.
  *
  * RNG MODES.  Every draw the reference takes from numpy's global MT19937 stream can either be
  * INJECTED (explicit arrays below: bit-exact parity with the reference given its draws) or taken

@@ -431,24 +431,26 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i) rewm[i] = 0u;
 
-    // ---- request expiry (core.py:303-306), 4 pickup points per op.  Run before the move: expiry
-    //      reads no positions and the move reads no requests, so the two commute, and the pickup
-    //      table is final before the move loop -- which lets its lookups be issued inside it.
+    // ---- request expiry (core.py:303-306), 4 pickup points per op.  Timer bytes hold the low 8
+    //      bits of the step at which the request expires (opened at t0 with wait W: t0 + W, the
+    //      step whose decrement would reach 0), so nothing is decremented; a request opened at
+    //      t0 >= 0 cannot expire before step W, so waves with every t < W skip the phase (with
+    //      T = W, 199 of 200 steps).  Run before the move: expiry reads no positions and the move
+    //      reads no requests, so the two commute, and the pickup table is final before the move
+    //      loop -- which lets its lookups be issued inside it.
     asm volatile("; PHASE expire" ::: "memory");
-    if (!(ablate & 4)) {
+    if (!(ablate & 4) && __any(t >= W)) {
+      const uint32_t tq = (t & 0xFFu) * 0x01010101u;
       uint32_t any_exp = 0;
 #pragma unroll
       for (int w = 0; w < C::PW; ++w) {
-        const uint32_t live = nz_hi(s.pt[w]);
-        const uint32_t tm = s.pm[w] - (live >> 7);
-        const uint32_t zero = ~((((tm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tm)) & 0x80808080u;
-        const uint32_t ex = zero & live;
-        const uint32_t m = (ex >> 7) * 0xFFu;
+        const uint32_t x = s.pm[w] ^ tq;   // zero byte: expires now
+        const uint32_t zero = ~((((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x)) & 0x80808080u;
+        const uint32_t ex = zero & nz_hi(s.pt[w]);
         any_exp |= ex;
-        s.pt[w] &= ~m;
-        s.pm[w] = tm & ~m;
+        s.pt[w] &= ~((ex << 1) - (ex >> 7));
       }
-      if (__any(any_exp != 0u)) s.am = active_mask(s);   // rare: only reset-time requests expire
+      if (__any(any_exp != 0u)) s.am = active_mask(s);
     }
 #pragma unroll
     for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
@@ -589,9 +591,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       }
 #pragma unroll
       for (int w = 0; w < C::PW; ++w) {
-        const uint32_t m = expand_nib((uint32_t)(picked >> (4 * w)) & 0xFu);
-        s.pt[w] &= ~m;
-        s.pm[w] &= ~m;
+        s.pt[w] &= ~expand_nib((uint32_t)(picked >> (4 * w)) & 0xFu);   // (timer bytes of closed
+                                                                        //  points are don't-care)
       }
       s.am &= ~picked;
     }
@@ -637,7 +638,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         }
       }
       if (__any(opened != 0ull)) {
-        const uint32_t wb = W * 0x01010101u;
+        const uint32_t wb = ((t + W) & 0xFFu) * 0x01010101u;   // expires at step t + W
 #pragma unroll
         for (int w = 0; w < C::PW; ++w) {
           const uint32_t m = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu);
@@ -1096,7 +1097,7 @@ __global__ __launch_bounds__(BT) void k_pack(PackParams a) {
       const int32_t tg = a.pickup_target[e * a.P + j];
       if (tg >= 0 && tg < DP) {
         tw |= (uint32_t)(tg + 1) << (8 * b);
-        mw |= ((uint32_t)a.pickup_timer[e * a.P + j] & 0xFFu) << (8 * b);
+        mw |= (((uint32_t)a.t[e] + (uint32_t)a.pickup_timer[e * a.P + j]) & 0xFFu) << (8 * b);   // expiry step
       }
     }
     a.state[(2 + a.na + w) * B + e] = tw;
@@ -1129,7 +1130,7 @@ __global__ __launch_bounds__(BT) void k_unpack(PackParams a) {
       const int j = 4 * w + b;
       const uint32_t tg = (tw >> (8 * b)) & 0xFFu;
       a.pickup_target[e * a.P + j] = (int32_t)tg - 1;
-      a.pickup_timer[e * a.P + j] = tg ? (int32_t)((mw >> (8 * b)) & 0xFFu) : -1;
+      a.pickup_timer[e * a.P + j] = tg ? (int32_t)(((mw >> (8 * b)) - h) & 0xFFu) : -1;   // steps left
     }
   }
 }
