@@ -102,20 +102,38 @@ struct Reader {
   }
 };
 
-__device__ __forceinline__ int select_bit64(uint64_t m, uint32_t r) {
-  uint32_t w = (uint32_t)m;
-  int base = 0;
-  uint32_t c = __popc(w);
-  if (r >= c) { r -= c; w = (uint32_t)(m >> 32); base = 32; }
-  c = __popc(w & 0xFFFFu);
-  if (r >= c) { r -= c; w >>= 16; base += 16; }
-  c = __popc(w & 0xFFu);
-  if (r >= c) { r -= c; w >>= 8; base += 8; }
-  c = __popc(w & 0xFu);
-  if (r >= c) { r -= c; w >>= 4; base += 4; }
-  c = __popc(w & 0x3u);
-  if (r >= c) { r -= c; w >>= 2; base += 2; }
-  if (r >= (w & 1u)) base += 1;
+// Branch-free selects without VCC: a one-wave-per-SIMD kernel pays for every v_cmp -> SGPR mask ->
+// v_cndmask round trip (measured: tools/oprate3.hip), while v_bitop3 is a plain full-rate VALU op.
+// Masks are 0 / 0xFFFFFFFF in VGPRs; every consumer goes through the bitop3 builtin so LLVM cannot
+// fold the mask arithmetic back into compare + select.
+constexpr uint32_t TA = 0xF0, TB = 0xCC, TC = 0xAA;   // truth-table columns of operands 0, 1, 2
+template <uint32_t TT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)(TT & 0xFFu));
+}
+__device__ __forceinline__ uint32_t mask_z(uint32_t x) { return (uint32_t)((int32_t)(x - 1u) >> 31); }   // x == 0 (x < 2^31)
+__device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { return bop3<(TA & TB) | (~TA & TC)>(m, a, b); }
+
+// Index of the r-th (0-based) set bit of m (r < popcount(m)).  Binary search over popcounts with
+// the rank kept as sr = -1 - r: popcount(x) + sr is negative exactly when r >= popcount(x), and is
+// then the rank left for the upper part.  Selects are v_bitop3 on sign masks (no VCC).
+__device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
+  uint32_t sr = ~r;
+  uint32_t u = (uint32_t)__popc((uint32_t)m) + sr;
+  uint32_t g = (uint32_t)((int32_t)u >> 31);
+  uint32_t w = msel(g, (uint32_t)(m >> 32), (uint32_t)m);
+  sr = msel(g, u, sr);
+  uint32_t base = bop3<TA & TB>(g, 32u, 0u);
+#pragma unroll
+  for (int k = 16; k >= 1; k >>= 1) {
+    u = (uint32_t)__popc(w & ((1u << k) - 1u)) + sr;
+    g = (uint32_t)((int32_t)u >> 31);
+    if (k > 1) {
+      w = msel(g, w >> k, w);
+      sr = msel(g, u, sr);
+    }
+    base = bop3<(TA & TB) | TC>(g, (uint32_t)k, base);
+  }
   return base;
 }
 
@@ -130,18 +148,6 @@ __device__ __forceinline__ uint32_t expand_nib(uint32_t nib) {
   const uint32_t ones = __umul24(nib, 0x00204081u) & 0x01010101u;
   return (ones << 8) - ones;
 }
-
-// Branch-free selects without VCC: a one-wave-per-SIMD kernel pays for every v_cmp -> SGPR mask ->
-// v_cndmask round trip (measured: tools/oprate3.hip), while v_bitop3 is a plain full-rate VALU op.
-// Masks are 0 / 0xFFFFFFFF in VGPRs; every consumer goes through the bitop3 builtin so LLVM cannot
-// fold the mask arithmetic back into compare + select.
-constexpr uint32_t TA = 0xF0, TB = 0xCC, TC = 0xAA;   // truth-table columns of operands 0, 1, 2
-template <uint32_t TT>
-__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)(TT & 0xFFu));
-}
-__device__ __forceinline__ uint32_t mask_z(uint32_t x) { return (uint32_t)((int32_t)(x - 1u) >> 31); }   // x == 0 (x < 2^31)
-__device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { return bop3<(TA & TB) | (~TA & TC)>(m, a, b); }
 
 // packed i16 max/min, pinned: hipcc rewrites clamp(x, -1, 1) on i16 pairs into per-half
 // compare/select cascades (it recognises sign(x)); one v_pk_* op per bound is what we want.
@@ -181,16 +187,18 @@ template <class C>
 struct Regs {
   uint32_t hdr, epi;
   uint32_t ag[C::NAM];
-  uint32_t pt[C::PW];
-  uint32_t pm[C::PW];
-  uint64_t am;   // open requests (derived from pt; kept in registers across fused steps)
+  uint64_t am;   // open requests (bit j = pickup point j has one; kept in registers across steps)
 };
 
 template <class C>
 struct Lds {
   uint32_t tbl[C::TBLW];
   uint32_t occ[C::D][BT];        // occupancy row y: bit x
-  uint32_t ptl[C::PW + 1][BT];   // pickup target bytes (+1 scratch word for predicated stores)
+  // Pickup point j of lane tid: low byte = request target + 1 (0 = none), high byte = expiry step
+  // (low 8 bits).  Row P is scratch: predicated stores of lanes with nothing to write go there.
+  // One 16-bit cell per (point, lane) makes every per-point access a single ds op whose address
+  // is j * BT + tid, and keeps the pickup table out of the VGPRs.
+  uint16_t pkp[C::P + 1][BT];
   uint32_t agl[C::NAM][BT];      // agent words when processing in action-dict order
   __device__ __forceinline__ uint32_t cell_pickup(uint32_t xy16) const {   // pickup index + 1 or 0
     return reinterpret_cast<const uint8_t*>(tbl)[(xy16 & 31u) | (xy16 >> 11)];
@@ -200,8 +208,11 @@ struct Lds {
   __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
   __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
   __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
-  __device__ __forceinline__ uint8_t* ptl_byte(uint32_t j, int tid) {
-    return reinterpret_cast<uint8_t*>(&ptl[j >> 2][tid]) + (j & 3u);
+  __device__ __forceinline__ uint32_t target_byte(uint32_t j, int tid) const {
+    return *reinterpret_cast<const uint8_t*>(&pkp[j][tid]);
+  }
+  __device__ __forceinline__ void clear_target(uint32_t j, int tid) {
+    *reinterpret_cast<uint8_t*>(&pkp[j][tid]) = 0;
   }
 };
 
@@ -211,10 +222,10 @@ __device__ __forceinline__ void load_tables(uint32_t* dst, const uint32_t* __res
 }
 
 template <class C>
-__device__ __forceinline__ uint64_t active_mask(const Regs<C>& s) {
+__device__ __forceinline__ uint64_t active_mask(const uint32_t (&pt)[C::PW]) {
   uint64_t am = 0;
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) am |= (uint64_t)nib_of(nz_hi(s.pt[w])) << (4 * w);
+  for (int w = 0; w < C::PW; ++w) am |= (uint64_t)nib_of(nz_hi(pt[w])) << (4 * w);
   return am;
 }
 
@@ -224,23 +235,27 @@ __device__ __forceinline__ uint64_t low_mask() {
 }
 
 template <class C>
-__device__ __forceinline__ void load_env(Regs<C>& s, const uint32_t* __restrict__ st, int64_t B,
-                                         int64_t e, int na) {
+__device__ __forceinline__ void load_env(Regs<C>& s, Lds<C>& L, const uint32_t* __restrict__ st, int64_t B,
+                                         int64_t e, int na, int tid) {
   s.hdr = st[e];
   s.epi = st[B + e];
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) s.ag[i] = (i < na) ? st[(2 + i) * B + e] : IDLE;
   const int wpt = 2 + na;
+  uint32_t pt[C::PW], pm[C::PW];
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) s.pt[w] = st[(wpt + w) * B + e];
+  for (int w = 0; w < C::PW; ++w) pt[w] = st[(wpt + w) * B + e];
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) s.pm[w] = st[(wpt + C::PW + w) * B + e];
-  s.am = active_mask(s);
+  for (int w = 0; w < C::PW; ++w) pm[w] = st[(wpt + C::PW + w) * B + e];
+#pragma unroll
+  for (int j = 0; j < C::P; ++j)
+    L.pkp[j][tid] = (uint16_t)(((pt[j >> 2] >> (8 * (j & 3))) & 0xFFu) | (((pm[j >> 2] >> (8 * (j & 3))) & 0xFFu) << 8));
+  s.am = active_mask<C>(pt);
 }
 
 template <class C>
-__device__ __forceinline__ void store_env(const Regs<C>& s, uint32_t* __restrict__ st, int64_t B,
-                                          int64_t e, int na) {
+__device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uint32_t* __restrict__ st,
+                                          int64_t B, int64_t e, int na, int tid) {
   st[e] = s.hdr;
   st[B + e] = s.epi;
 #pragma unroll
@@ -248,9 +263,17 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, uint32_t* __restrict
     if (i < na) st[(2 + i) * B + e] = s.ag[i];
   const int wpt = 2 + na;
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) st[(wpt + w) * B + e] = s.pt[w];
+  for (int w = 0; w < C::PW; ++w) {
+    uint32_t pt = 0, pm = 0;
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) st[(wpt + C::PW + w) * B + e] = s.pm[w];
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t v = L.pkp[4 * w + b][tid];
+      pt |= (v & 0xFFu) << (8 * b);
+      pm |= (v >> 8) << (8 * b);
+    }
+    st[(wpt + w) * B + e] = pt;
+    st[(wpt + C::PW + w) * B + e] = pm;
+  }
 }
 
 // ----------------------------------------------------------------------------- reset
@@ -272,7 +295,8 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
     s.ag[i] = a;
   }
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = 0u;
+  for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+  const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
   uint64_t remP = low_mask<C::P>(), remD = low_mask<C::DP>();
   for (int j = 0; j < C::R; ++j) {
     const uint32_t r1 = __umulhi(rd.word(1 + na + 2 * j), (uint32_t)(C::P - j));
@@ -281,16 +305,9 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
     const uint32_t r2 = __umulhi(rd.word(2 + na + 2 * j), (uint32_t)(C::DP - j));
     const int tg = select_bit64(remD, r2);
     remD &= ~(1ull << tg);
-    *L.ptl_byte((uint32_t)sel, tid) = (uint8_t)(tg + 1);
+    L.pkp[sel][tid] = (uint16_t)((uint32_t)(tg + 1) | wexp);
   }
-  const uint64_t opened = low_mask<C::P>() & ~remP;
-  const uint32_t wb = W * 0x01010101u;
-#pragma unroll
-  for (int w = 0; w < C::PW; ++w) {
-    s.pt[w] = L.ptl[w][tid];
-    s.pm[w] = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu) & wb;
-  }
-  s.am = opened;
+  s.am = low_mask<C::P>() & ~remP;
   s.hdr = (n << 16) | (1u << 24);
   s.epi = ep;
 }
@@ -312,20 +329,15 @@ __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e,
     s.ag[i] = a;
   }
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = 0u;
+  for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+  const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
   uint64_t opened = 0;
   for (int j = 0; j < C::R; ++j) {
     const uint32_t sel = (uint32_t)pickups[e * C::R + j];
     const uint32_t tg = (uint32_t)targets[e * C::R + j];
     if (sel >= (uint32_t)C::P || tg >= (uint32_t)C::DP) continue;   // invalid injected draw: ignored
     opened |= 1ull << sel;
-    *L.ptl_byte(sel, tid) = (uint8_t)(tg + 1);
-  }
-  const uint32_t wb = W * 0x01010101u;
-#pragma unroll
-  for (int w = 0; w < C::PW; ++w) {
-    s.pt[w] = L.ptl[w][tid];
-    s.pm[w] = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu) & wb;
+    L.pkp[sel][tid] = (uint16_t)((tg + 1u) | wexp);
   }
   s.am = opened;
   s.hdr = (n << 16) | (1u << 24);
@@ -440,20 +452,16 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     //      loop -- which lets its lookups be issued inside it.
     asm volatile("; PHASE expire" ::: "memory");
     if (!(ablate & 4) && __any(t >= W)) {
-      const uint32_t tq = (t & 0xFFu) * 0x01010101u;
-      uint32_t any_exp = 0;
+      uint64_t expired = 0;
 #pragma unroll
-      for (int w = 0; w < C::PW; ++w) {
-        const uint32_t x = s.pm[w] ^ tq;   // zero byte: expires now
-        const uint32_t zero = ~((((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x)) & 0x80808080u;
-        const uint32_t ex = zero & nz_hi(s.pt[w]);
-        any_exp |= ex;
-        s.pt[w] &= ~((ex << 1) - (ex >> 7));
+      for (int j = 0; j < C::P; ++j) {
+        const uint32_t v = L.pkp[j][tid];
+        const bool ex = (v & 0xFFu) != 0u && (v >> 8) == (t & 0xFFu);
+        if (ex) L.clear_target(j, tid);
+        expired |= (uint64_t)ex << j;
       }
-      if (__any(any_exp != 0u)) s.am = active_mask(s);
+      s.am &= ~expired;
     }
-#pragma unroll
-    for (int w = 0; w < C::PW; ++w) L.ptl[w][tid] = s.pt[w];
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
     asm volatile("; PHASE move" ::: "memory");
@@ -554,10 +562,10 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           s.ag[sidx] = moved;
           mokp = mok;
           cp[sidx] = L.cell_pickup(moved & XY16);
-          if (sidx >= 1) tb[sidx - 1] = *L.ptl_byte(min(cp[sidx - 1] - 1u, (uint32_t)(4 * C::PW)), tid);
+          if (sidx >= 1) tb[sidx - 1] = L.target_byte(min(cp[sidx - 1] - 1u, (uint32_t)C::P), tid);
           if (sidx >= 2) dst[sidx - 2] = L.dst((tb[sidx - 2] - 1u) & 63u);
         }
-        tb[C::NAM - 1] = *L.ptl_byte(min(cp[C::NAM - 1] - 1u, (uint32_t)(4 * C::PW)), tid);
+        tb[C::NAM - 1] = L.target_byte(min(cp[C::NAM - 1] - 1u, (uint32_t)C::P), tid);
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst((tb[C::NAM - 2] - 1u) & 63u);
         dst[C::NAM - 1] = L.dst((tb[C::NAM - 1] - 1u) & 63u);
         looked = true;
@@ -572,7 +580,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
 #pragma unroll
-        for (int i = 0; i < C::NAM; ++i) tb[i] = *L.ptl_byte(min(cp[i] - 1u, (uint32_t)(4 * C::PW)), tid);
+        for (int i = 0; i < C::NAM; ++i) tb[i] = L.target_byte(min(cp[i] - 1u, (uint32_t)C::P), tid);
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
       }
@@ -582,17 +590,14 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         // take iff on a pickup point (cp != 0) with an open request (tb != 0) and idle: slots >= n
         // sit idle on the corner cell (0, 0), which is no pickup point.  min3 of the three 0/1-ish
         // terms is 1 exactly when all hold.
+        // The point is cleared right away: every agent's target byte was read before this loop.
         const uint32_t a = s.ag[i];
-        const uint32_t idle01 = ((a & 0xFF00u) + 0x100u) >> 16;
+        const uint32_t idle01 = (a >> 15) & 1u;   // delivery-target byte 0xFF
         const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cp[i], tb[i]), idle01);
         s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dst[i] << 8, IDLE);   // idle target bytes are 0xFF
         picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cp[i] - 1u) & 63u);
+        L.clear_target(msel(m, cp[i] - 1u, (uint32_t)C::P), tid);   // row P: scratch
         rewm[i] = m;
-      }
-#pragma unroll
-      for (int w = 0; w < C::PW; ++w) {
-        s.pt[w] &= ~expand_nib((uint32_t)(picked >> (4 * w)) & 0xFu);   // (timer bytes of closed
-                                                                        //  points are don't-care)
       }
       s.am &= ~picked;
     }
@@ -607,45 +612,47 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     if (phase == PH_PRE) {
       if (n_inactive) n_inactive[e] = (int32_t)nin;
     } else {
-      uint64_t rem = inactive, used = 0, opened = 0;
+      // 64-bit sets as (lo, hi) halves so that every mask consumer is a v_bitop3
+      uint32_t rlo = (uint32_t)inactive, rhi = (uint32_t)(inactive >> 32);   // still selectable
+      uint32_t ulo = 0, uhi = 0;                                               // targets used
+      uint32_t olo = 0, ohi = 0;                                               // points opened
       uint32_t first_t = 0;
+      const uint32_t wexp = ((t + W) & 0xFFu) << 8;   // expires at step t + W
       uint4 blk = make_uint4(0u, 0u, 0u, 0u);   // words 2j (pickup) and 2j+1 (target) share a block
 #pragma unroll
       for (int j = 0; j < C::R; ++j) {
         if (__any(j < kreq)) {                  // wave-uniform: skip items no env needs
-          const bool act_j = j < kreq;
-          int sel, tgi;
+          uint32_t ma = (uint32_t)((int32_t)((uint32_t)j - (uint32_t)kreq) >> 31);   // j < kreq
+          uint32_t sel, tgi;
           if (regen) {
-            const uint32_t rpos = act_j ? (uint32_t)regen[e * 2 * C::R + j] : 0u;
-            tgi = act_j ? regen[e * 2 * C::R + C::R + j] : 0;
-            sel = (rpos < nin && (uint32_t)tgi < (uint32_t)C::DP) ? select_bit64(inactive, rpos) : C::P;
+            const uint32_t rpos = (uint32_t)regen[e * 2 * C::R + j];
+            tgi = (uint32_t)regen[e * 2 * C::R + C::R + j];
+            const bool valid = rpos < nin && tgi < (uint32_t)C::DP;   // invalid draws are ignored
+            ma = bop3<TA & TB>(ma, 0u - (uint32_t)valid, 0u);
+            sel = select_bit64(inactive, rpos);   // positions into the inactive list, host-drawn
           } else {
             if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
             const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
-            sel = select_bit64(rem, __umulhi(w1, nin - (uint32_t)j));
+            sel = select_bit64(((uint64_t)rhi << 32) | rlo, __umulhi(w1, nin - (uint32_t)j));
             const uint32_t r2 = __umulhi(w2, (uint32_t)(C::DP - j));
-            if (j == 0) tgi = (int)r2;                                   // nothing used yet
-            else if (j == 1) tgi = (int)(r2 + (r2 >= first_t ? 1u : 0u));  // one point removed
-            else tgi = select_bit64(~used & low_mask<C::DP>(), r2);
+            if (j == 0) tgi = r2;                                               // nothing used yet
+            else if (j == 1) tgi = r2 + ((first_t - 1u - r2) >> 31);   // + (r2 >= first): skip it
+            else tgi = select_bit64(~(((uint64_t)uhi << 32) | ulo) & low_mask<C::DP>(), r2);
             if (j == 0) first_t = r2;
           }
-          const bool apply = act_j && sel < C::P;
-          rem &= apply ? ~(1ull << (sel & 63)) : ~0ull;
-          used |= apply ? (1ull << (tgi & 63)) : 0ull;
-          opened |= apply ? (1ull << (sel & 63)) : 0ull;
-          // predicated byte store: inactive lanes write the scratch word
-          *L.ptl_byte(apply ? (uint32_t)sel : (uint32_t)(4 * C::PW), tid) = (uint8_t)(tgi + 1);
+          const uint64_t sb = 1ull << (sel & 63u), tb64 = 1ull << (tgi & 63u);
+          const uint32_t slo = bop3<TA & TB>(ma, (uint32_t)sb, 0u), shi = bop3<TA & TB>(ma, (uint32_t)(sb >> 32), 0u);
+          rlo &= ~slo;
+          rhi &= ~shi;
+          olo |= slo;
+          ohi |= shi;
+          ulo = bop3<(TA & TB) | TC>(ma, (uint32_t)tb64, ulo);
+          uhi = bop3<(TA & TB) | TC>(ma, (uint32_t)(tb64 >> 32), uhi);
+          // predicated store: lanes with nothing to open write the scratch row
+          L.pkp[msel(ma, sel, (uint32_t)C::P)][tid] = (uint16_t)((tgi + 1u) | wexp);
         }
       }
-      if (__any(opened != 0ull)) {
-        const uint32_t wb = ((t + W) & 0xFFu) * 0x01010101u;   // expires at step t + W
-#pragma unroll
-        for (int w = 0; w < C::PW; ++w) {
-          const uint32_t m = expand_nib((uint32_t)(opened >> (4 * w)) & 0xFu);
-          s.pt[w] = (s.pt[w] & ~m) | (L.ptl[w][tid] & m);
-          s.pm[w] = (s.pm[w] & ~m) | (wb & m);
-        }
-      }
+      const uint64_t opened = ((uint64_t)ohi << 32) | olo;
       s.am |= opened;
     }
   }
@@ -779,7 +786,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const Keys k{a.k0, a.k1};
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
-  load_env<C>(s, a.state, a.B, e, a.na);
+  load_env<C>(s, L, a.state, a.B, e, a.na, tid);
   // Drain the state loads here.  Their first uses are inside the step loop, so otherwise the
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
@@ -843,7 +850,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   }
   if (a.returns) a.returns[e] += ret;
   if (stats) a.stats.episode_return[e] = epr;
-  store_env<C>(s, a.state, a.B, e, a.na);
+  store_env<C>(s, L, a.state, a.B, e, a.na, tid);
 }
 
 struct ResetParams {
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
   else
     reset_philox<C>(s, L, Keys{a.k0, a.k1}, (uint32_t)(a.env_offset + e), a.na, a.variable_n,
                     (uint32_t)a.W, tid);
-  store_env<C>(s, a.state, a.B, e, a.na);
+  store_env<C>(s, L, a.state, a.B, e, a.na, tid);
 }
 
 // Observation rows (core.py:371-432, reset rows core.py:224-260), HBM-write bound.
