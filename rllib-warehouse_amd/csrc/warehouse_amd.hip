@@ -33,6 +33,7 @@
 namespace {
 
 constexpr int BT = 256;  // lanes (= envs) per workgroup
+constexpr uint32_t ROWB = 2 * BT;   // bytes per pickup-point row of the LDS pickup plane
 
 enum Policy { POL_EXTERNAL = 0, POL_GREEDY = 1, POL_RANDOM = 2 };
 enum Purpose : uint32_t { PUR_RESET = 1, PUR_REGEN = 2, PUR_POLICY = 3, PUR_RANDOM = 4 };
@@ -45,9 +46,9 @@ constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 struct TableLayout {
   int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
-      : cell(0), rp(32 * D), tag(32 * D + 4 * (P + 1)), dst(32 * D + 8 * (P + 1)),
-        mv(32 * D + 8 * (P + 1) + 4 * DP), valid(32 * D + 8 * (P + 1) + 4 * DP + 48),
-        bytes(32 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
+      : cell(0), rp(512 * D), tag(512 * D + 4 * (P + 1)), dst(512 * D + 8 * (P + 1)),
+        mv(512 * D + 8 * (P + 1) + 4 * DP), valid(512 * D + 8 * (P + 1) + 4 * DP + 48),
+        bytes(512 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
 
 template <int D_, int R_, int NR_, int NAM_>
@@ -200,9 +201,13 @@ struct Lds {
   // is j * BT + tid, and keeps the pickup table out of the VGPRs.
   uint16_t pkp[C::P + 1][BT];
   uint32_t agl[C::NAM][BT];      // agent words when processing in action-dict order
-  __device__ __forceinline__ uint32_t cell_pickup(uint32_t xy16) const {   // pickup index + 1 or 0
-    return reinterpret_cast<const uint8_t*>(tbl)[(xy16 & 31u) | (xy16 >> 11)];
+  // Cell (x | y << 16) -> (pickup index + 1) * ROWB, 0 for other cells: the byte offset of the
+  // point's row in pkp, counted from the row before it, so a lookup is one v_perm + one ds_read
+  // and the dependent target read one add.
+  __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
+    return reinterpret_cast<const uint16_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
   }
+
   __device__ __forceinline__ uint32_t rp(uint32_t j) const { return tbl[C::T.rp / 4 + j]; }
   __device__ __forceinline__ uint32_t tag(uint32_t j) const { return tbl[C::T.tag / 4 + j]; }
   __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
@@ -214,6 +219,18 @@ struct Lds {
   __device__ __forceinline__ void clear_target(uint32_t j, int tid) {
     *reinterpret_cast<uint8_t*>(&pkp[j][tid]) = 0;
   }
+  // Target byte addressed by a cell_row() value (0: the row before pkp -- garbage, never used).
+  __device__ __forceinline__ uint32_t pkp_offset() const {
+    return (uint32_t)(reinterpret_cast<const char*>(&pkp[0][0]) - reinterpret_cast<const char*>(this));
+  }
+  __device__ __forceinline__ const uint8_t* row_byte(uint32_t cv, int tid) const {
+    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv + 2 * tid;
+  }
+  __device__ __forceinline__ uint8_t* row_byte(uint32_t cv, int tid) {
+    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv + 2 * tid;
+  }
+  // delivery cell of a target byte (target + 1; 0 reads the word before the table: never used)
+  __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const { return tbl[C::T.dst / 4 - 1 + tb]; }
 };
 
 template <class C>
@@ -465,7 +482,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
     asm volatile("; PHASE move" ::: "memory");
-    uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329)
+    uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329): cell_row,
+                                                    // target byte, delivery cell
     bool looked = false;
     if (!(ablate & 2)) {
       // The grid is rebuilt as {live agents' cells} (core.py:275-276) by OR-ing the cells into
@@ -561,13 +579,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
           s.ag[sidx] = moved;
           mokp = mok;
-          cp[sidx] = L.cell_pickup(moved & XY16);
-          if (sidx >= 1) tb[sidx - 1] = L.target_byte(min(cp[sidx - 1] - 1u, (uint32_t)C::P), tid);
-          if (sidx >= 2) dst[sidx - 2] = L.dst((tb[sidx - 2] - 1u) & 63u);
+          cp[sidx] = L.cell_row(moved);
+          if (sidx >= 1) tb[sidx - 1] = *L.row_byte(cp[sidx - 1], tid);
+          if (sidx >= 2) dst[sidx - 2] = L.dst_tb(tb[sidx - 2]);
         }
-        tb[C::NAM - 1] = L.target_byte(min(cp[C::NAM - 1] - 1u, (uint32_t)C::P), tid);
-        if (C::NAM >= 2) dst[C::NAM - 2] = L.dst((tb[C::NAM - 2] - 1u) & 63u);
-        dst[C::NAM - 1] = L.dst((tb[C::NAM - 1] - 1u) & 63u);
+        tb[C::NAM - 1] = *L.row_byte(cp[C::NAM - 1], tid);
+        if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
+        dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
         looked = true;
       }
     }
@@ -578,11 +596,11 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     if (!(ablate & 8)) {
       if (!looked) {
 #pragma unroll
-        for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_pickup(s.ag[i] & XY16);
+        for (int i = 0; i < C::NAM; ++i) cp[i] = L.cell_row(s.ag[i]);
 #pragma unroll
-        for (int i = 0; i < C::NAM; ++i) tb[i] = L.target_byte(min(cp[i] - 1u, (uint32_t)C::P), tid);
+        for (int i = 0; i < C::NAM; ++i) tb[i] = *L.row_byte(cp[i], tid);
 #pragma unroll
-        for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst((tb[i] - 1u) & 63u);
+        for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst_tb(tb[i]);
       }
       uint64_t picked = 0;
 #pragma unroll
@@ -595,8 +613,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         const uint32_t idle01 = (a >> 15) & 1u;   // delivery-target byte 0xFF
         const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cp[i], tb[i]), idle01);
         s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dst[i] << 8, IDLE);   // idle target bytes are 0xFF
-        picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cp[i] - 1u) & 63u);
-        L.clear_target(msel(m, cp[i] - 1u, (uint32_t)C::P), tid);   // row P: scratch
+        picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cp[i] / ROWB - 1u) & 63u);
+        *L.row_byte(msel(m, cp[i], (uint32_t)(C::P + 1) * ROWB), tid) = 0;   // row P: scratch
         rewm[i] = m;
       }
       s.am &= ~picked;
@@ -680,13 +698,29 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 }
 
 // ----------------------------------------------------------------------------- kernels
-// rewards[B, na]: a wave's 64 envs own one contiguous block of 64*na floats.  Lanes write their
-// rows into LDS (the agl scratch, free after the move phase) and read the block back so every
-// global store instruction writes contiguous 16-byte lanes (1 KiB per wave-instruction) instead
-// of one strided row per lane.
+// rewards[B, na]: a wave's 64 envs own one contiguous block of 64*na floats.  Even agent counts
+// store each lane's row with 16/8-byte stores; otherwise lanes write their rows into LDS (the agl
+// scratch, free after the move phase) and read the block back so every global store instruction
+// writes contiguous 16-byte lanes instead of one strided row per lane.
 template <class C>
 __device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::NAM], float* out,
                                               int64_t B, int64_t e, int na, int tid, bool direct) {
+  if ((C::NAM & 1) == 0 && na == C::NAM && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    // One row of 16-byte (8-byte) stores per lane: the two wave-instructions of a Medium-8 step
+    // cover the wave's contiguous 2 KiB block between them (A/B: 5 % faster than the LDS transpose
+    // below, whose row writes are 8-way bank conflicts).
+    if ((C::NAM & 3) == 0) {
+      float4* row = reinterpret_cast<float4*>(out + e * na);
+#pragma unroll
+      for (int q = 0; q < C::NAM / 4; ++q)
+        row[q] = make_float4(rew[4 * q], rew[4 * q + 1], rew[4 * q + 2], rew[4 * q + 3]);
+    } else {
+      float2* row = reinterpret_cast<float2*>(out + e * na);
+#pragma unroll
+      for (int q = 0; q < C::NAM / 2; ++q) row[q] = make_float2(rew[2 * q], rew[2 * q + 1]);
+    }
+    return;
+  }
   const int lane = tid & 63;
   const int64_t e0 = e - lane;
   // tail wave (lanes past B have exited) or masked step (unstepped lanes have exited): no
@@ -1171,7 +1205,7 @@ int validate(const wh_config* c, Geometry* g) {
 }
 
 // Host copy of the per-workgroup tables, same layout as TableLayout (core.py:170-199):
-//   cell  [32*D] u8  : (x | y << 5) -> pickup index + 1, 0 = not a pickup cell
+//   cell  [256*D] u16: (x | y << 8) -> (pickup index + 1) * ROWB, 0 = not a pickup cell
 //   rp    [P+1]  u32 : pickup cell as x | y << 16; [P] = far-away cell (never nearest)
 //   tag   [P+1]  u32 : pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58);
 //                      [P] = the null cell (D/2, D/2): where fresh-reset agents head (core.py:233-236)
@@ -1182,7 +1216,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   const int D = g.D;
   *bad = 0;
   if (D > 32) { *bad = 1; return {}; }
-  std::vector<uint8_t> cell(32 * D, 0);
+  std::vector<uint16_t> cell(256 * D, 0);
   std::vector<uint32_t> rp(g.P + 1), tag(g.P + 1);
   rp[g.P] = 0x00FF00FFu;
   tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);
@@ -1191,8 +1225,8 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
       for (int q = 0; q < 4; ++q) {
         const int j = (ix * g.NR + iy) * 4 + q;
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
-        if (cell[x | (y << 5)]) *bad = 1;  // overlapping racks
-        cell[x | (y << 5)] = (uint8_t)(j + 1);
+        if (cell[x | (y << 8)]) *bad = 1;  // overlapping racks
+        cell[x | (y << 8)] = (uint16_t)((j + 1) * ROWB);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
         tag[j] = ((uint32_t)j << 10) | ((uint32_t)x << 5) | (uint32_t)y;
       }
@@ -1211,9 +1245,9 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   std::vector<uint32_t> valid;
   for (int x = 1; x < D - 1; ++x)
     for (int y = 1; y < D - 1; ++y)
-      if (!cell[x | (y << 5)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
-  std::vector<uint32_t> words((cell.size() + 3) / 4, 0);
-  memcpy(words.data(), cell.data(), cell.size());
+      if (!cell[x | (y << 8)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
+  std::vector<uint32_t> words(cell.size() / 2, 0);
+  memcpy(words.data(), cell.data(), cell.size() * 2);
   words.insert(words.end(), rp.begin(), rp.end());
   words.insert(words.end(), tag.begin(), tag.end());
   words.insert(words.end(), dst.begin(), dst.end());
