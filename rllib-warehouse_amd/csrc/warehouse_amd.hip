@@ -414,7 +414,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
 #pragma unroll
       for (int r = 0; r < C::R; ++r)   // key = dist << 16 | pickup << 10 | x << 5 | y
         best = min(best, __builtin_amdgcn_sad_hi_u8(pos, rp[r], tg[r]));
-      const uint32_t near = ((best >> 5) & 31u) | ((best & 31u) << 16);
+      const uint32_t near = (((best >> 5) & 31u) | (best << 16)) & 0x001F001Fu;   // tag (x, y) -> x | y << 16
       const uint32_t dst = (a >> 8) & XY16;
       const uint32_t idle = (uint32_t)__builtin_amdgcn_sbfe((int)a, 15, 1);   // target byte 0xFF
       const uint32_t goal = msel(idle, near, dst);
@@ -501,7 +501,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
       }
       // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
-      uint32_t kk[3 * C::NAM];
+      uint32_t kk[3 * C::NAM];   // ORDERED path: 3 ordered keys per accepted move
+      uint32_t rk[C::NAM], xk[C::NAM];   // ascending path: reverse key, crossing pair
       if (ORDERED) {   // drop-in single env: agents in action-dict order, records in LDS
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
@@ -559,10 +560,14 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokp, set31, bop3<TC & ~(TA & TB)>(mokp, clr31, occ31));
           }
           if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
+          // forbidden moves (core.py:293-297): the reverse of every accepted move, matched as an
+          // ordered (from, to) key, and for accepted diagonals the two crossing moves, matched as
+          // one unordered cell pair ({from, to} == {c1, c2} is exactly "either crossing move")
           const uint32_t key = p | (c << 8);
+          const uint32_t ukey = min(p, c) | (max(p, c) << 8);
           uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
 #pragma unroll
-          for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
+          for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
           const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
           const uint32_t mok = (uint32_t)((int32_t)bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u) >> 31);
           atomicAnd(&L.occ[p >> 16][tid], bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
@@ -573,9 +578,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           const uint32_t mdiag = (uint32_t)((int32_t)bop3<TA & TB & TC>(nzh, nzh << 16, mok) >> 31);
           const uint32_t c1 = bop3<(TA & TC) | (TB & ~TC)>(c, p, 0xFFFFu);   // (cx, py)
           const uint32_t c2 = bop3<(TA & TC) | (TB & ~TC)>(p, c, 0xFFFFu);   // (px, cy)
-          kk[3 * sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
-          kk[3 * sidx + 1] = bop3<~TA | TB>(mdiag, c1 | (c2 << 8), 0u);
-          kk[3 * sidx + 2] = bop3<~TA | TB>(mdiag, c2 | (c1 << 8), 0u);
+          rk[sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
+          xk[sidx] = bop3<~TA | TB>(mdiag, min(c1, c2) | (max(c1, c2) << 8), 0u);
           const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
           s.ag[sidx] = moved;
           mokp = mok;
@@ -1225,8 +1229,9 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
       for (int q = 0; q < 4; ++q) {
         const int j = (ix * g.NR + iy) * 4 + q;
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
-        if (cell[x | (y << 8)]) *bad = 1;  // overlapping racks
-        cell[x | (y << 8)] = (uint16_t)((j + 1) * ROWB);
+        const int ci = x | (y << 8);
+        if (cell[ci]) *bad = 1;  // overlapping racks
+        cell[ci] = (uint16_t)((j + 1) * ROWB);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
         tag[j] = ((uint32_t)j << 10) | ((uint32_t)x << 5) | (uint32_t)y;
       }
