@@ -162,6 +162,11 @@ __device__ __forceinline__ uint32_t pk_min_i16(uint32_t a, uint32_t b) {
   asm("v_pk_min_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(ushort2v, a),
+                                                                __builtin_bit_cast(ushort2v, b)));
+}
 __device__ __forceinline__ uint32_t pk_sub_i16(uint32_t a, uint32_t b) {
   uint32_t r;
   asm("v_pk_sub_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -561,10 +566,15 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           }
           if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
           // forbidden moves (core.py:293-297): the reverse of every accepted move, matched as an
-          // ordered (from, to) key, and for accepted diagonals the two crossing moves, matched as
-          // one unordered cell pair ({from, to} == {c1, c2} is exactly "either crossing move")
+          // ordered (from, to) key, and for accepted diagonals the two crossing moves.  A move's
+          // square key is the low corner of the 2x2 square it spans plus 2*dx*dy in the top byte
+          // (+2 one diagonal, -2 the other, 0 straight or stay); "either crossing move of i" is
+          // exactly "same square, opposite diagonal", i.e. square key == i's with the top byte
+          // flipped (^ 0xFC000000), which no straight move's key ever equals.
           const uint32_t key = p | (c << 8);
-          const uint32_t ukey = min(p, c) | (max(p, c) << 8);
+          const uint32_t dd = pk_sub_i16(c, p);
+          const int ddot = __builtin_amdgcn_sdot2(as_s2(dd), as_s2(__builtin_amdgcn_alignbit(dd, dd, 16)), 0, false);
+          const uint32_t ukey = pk_min_u16(p, c) + ((uint32_t)ddot << 24);
           uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
 #pragma unroll
           for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
@@ -573,13 +583,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           atomicAnd(&L.occ[p >> 16][tid], bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
           atomicOr(&L.occ[c >> 16][tid], bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
           const uint32_t dxy = c ^ p;
-          // diagonal: both 16-bit halves of dxy nonzero (bit 15 of each half after + 0x7FFF)
-          const uint32_t nzh = dxy + 0x7FFF7FFFu;
-          const uint32_t mdiag = (uint32_t)((int32_t)bop3<TA & TB & TC>(nzh, nzh << 16, mok) >> 31);
-          const uint32_t c1 = bop3<(TA & TC) | (TB & ~TC)>(c, p, 0xFFFFu);   // (cx, py)
-          const uint32_t c2 = bop3<(TA & TC) | (TB & ~TC)>(p, c, 0xFFFFu);   // (px, cy)
           rk[sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
-          xk[sidx] = bop3<~TA | TB>(mdiag, min(c1, c2) | (max(c1, c2) << 8), 0u);
+          xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFC000000u);
           const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
           s.ag[sidx] = moved;
           mokp = mok;
