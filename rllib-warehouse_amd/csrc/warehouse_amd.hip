@@ -817,6 +817,67 @@ __device__ __forceinline__ void flush_episodes(bool fin, uint32_t n, uint32_t re
   }
 }
 
+// The step loop of k_step.  PHASE >= 0 fixes the phase at compile time (the fused rollout and the
+// sampler path run PH_ALL), so the phase tests fold away and each step is a few large basic blocks
+// the scheduler can interleave; -1 reads it from the launch (the drop-in's split step).  Phase
+// ablation (tools/ablate.py) exists only in builds with -DWH_ABLATION.
+template <class C, int POLICY, bool ORDERED, int PHASE>
+__device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C>& L, const Keys& k,
+                                          uint32_t gid, int64_t e, int tid) {
+  const int phase = PHASE >= 0 ? PHASE : a.phase;
+#ifdef WH_ABLATION
+  const int ablate = a.ablate;
+#else
+  constexpr int ablate = 0;
+#endif
+  float ret = 0.0f;
+  const bool stats = a.stats.episode_return != nullptr;
+  uint32_t epr = stats ? a.stats.episode_return[e] : 0u;
+  for (int stp = 0; stp < a.steps; ++stp) {
+    uint32_t d[C::NAM];
+    if (POLICY == POL_EXTERNAL) {
+      const bool have = phase != PH_REGEN && !ORDERED;   // REGEN reads no actions
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) {
+        uint32_t mv = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
+        d[i] = L.mv(mv > 8u ? 4u : mv);
+      }
+    } else if (ablate & 1) {
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
+    } else {
+      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+    }
+    float rew[C::NAM];
+    const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, phase,
+                                  (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, ablate);
+    if (phase != PH_REGEN) {
+      if (a.rewards && !(ablate & 64))
+        store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid, a.mask != nullptr);
+      if (a.dones && !(ablate & 64)) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
+      if (a.returns) {
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) ret += rew[i];
+      }
+      if (stats) {
+        float r = 0.0f;
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) r += rew[i];   // whole numbers: exact
+        epr += (uint32_t)r;
+        if (__any(done)) flush_episodes(done, (s.hdr >> 16) & 0xFFu, epr, a.stats);
+        if (done) epr = 0;
+      }
+      if (done && a.autoreset && !(ablate & 128)) {
+        reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
+#pragma unroll
+        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+      }
+    }
+  }
+  if (a.returns) a.returns[e] += ret;
+  if (stats) a.stats.episode_return[e] = epr;
+}
+
 template <class C, int POLICY, bool ORDERED>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
@@ -847,52 +908,10 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     return;
   }
 
-  float ret = 0.0f;
-  const bool stats = a.stats.episode_return != nullptr;
-  uint32_t epr = stats ? a.stats.episode_return[e] : 0u;
-  for (int stp = 0; stp < a.steps; ++stp) {
-    uint32_t d[C::NAM];
-    if (POLICY == POL_EXTERNAL) {
-      const bool have = a.phase != PH_REGEN && !ORDERED;   // REGEN reads no actions
-#pragma unroll
-      for (int i = 0; i < C::NAM; ++i) {
-        uint32_t mv = (have && i < a.na) ? (uint32_t)a.actions[e * a.na + i] : 4u;
-        d[i] = L.mv(mv > 8u ? 4u : mv);
-      }
-    } else if (a.ablate & 1) {
-#pragma unroll
-      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
-    } else {
-      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
-    }
-    float rew[C::NAM];
-    const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, a.phase,
-                                  (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, a.ablate);
-    if (a.phase != PH_REGEN) {
-      if (a.rewards && !(a.ablate & 64))
-        store_rewards<C>(L, rew, a.rewards + (int64_t)stp * a.B * a.na, a.B, e, a.na, tid, a.mask != nullptr);
-      if (a.dones && !(a.ablate & 64)) a.dones[(int64_t)stp * a.B + e] = done ? 1 : 0;
-      if (a.returns) {
-#pragma unroll
-        for (int i = 0; i < C::NAM; ++i) ret += rew[i];
-      }
-      if (stats) {
-        float r = 0.0f;
-#pragma unroll
-        for (int i = 0; i < C::NAM; ++i) r += rew[i];   // whole numbers: exact
-        epr += (uint32_t)r;
-        if (__any(done)) flush_episodes(done, (s.hdr >> 16) & 0xFFu, epr, a.stats);
-        if (done) epr = 0;
-      }
-      if (done && a.autoreset && !(a.ablate & 128)) {
-        reset_philox<C>(s, L, k, gid, a.na, a.variable_n, (uint32_t)a.W, tid);
-#pragma unroll
-        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
-      }
-    }
-  }
-  if (a.returns) a.returns[e] += ret;
-  if (stats) a.stats.episode_return[e] = epr;
+  if (!ORDERED && a.phase == PH_ALL)
+    run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+  else
+    run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
   store_env<C>(s, L, a.state, a.B, e, a.na, tid);
 }
 

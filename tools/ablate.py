@@ -1,4 +1,6 @@
 """Phase-ablation timing of the fused step kernel (timing only: results are wrong by design).
+Needs the ablation build: bash tools/build_variant.sh ablation -DWH_ABLATION, then run with
+WAREHOUSE_AMD_LIB=build_ab/ablation.so (the production library compiles the ablation switches out).
 WH_ABLATE bits: 1 policy, 2 move, 4 expiry, 8 pickup, 16 regeneration, 32 delivery, 64 reward/done
 stores, 128 auto-reset."""
 import os

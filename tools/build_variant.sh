@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build a variant of the library for same-box A/B runs (tools/ab.sh):
 #   bash tools/build_variant.sh NAME [extra hipcc flags...]   ->  build_ab/NAME.so
+# e.g. the phase-ablation build tools/ablate.py needs: bash tools/build_variant.sh ablation -DWH_ABLATION
 cd "$(dirname "$0")/../rllib-warehouse_amd/csrc" || exit 2
 NAME=$1; shift
 mkdir -p ../../build_ab
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-function -I../../include \
-  "$@" warehouse_amd.hip policy_mlp.hip -o ../../build_ab/$NAME.so
+make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*"
