@@ -112,7 +112,14 @@ template <uint32_t TT>
 __device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)(TT & 0xFFu));
 }
-__device__ __forceinline__ uint32_t mask_z(uint32_t x) { return (uint32_t)((int32_t)(x - 1u) >> 31); }   // x == 0 (x < 2^31)
+// Sign bit -> 0 / all-ones.  As inline asm: LLVM turns ashr(a - b, 31) into a carry-out compare
+// plus v_cndmask (the round trip this file avoids).
+__device__ __forceinline__ uint32_t sgn(uint32_t x) {
+  uint32_t r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t mask_z(uint32_t x) { return sgn(x - 1u); }   // x == 0 (x < 2^31)
 __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { return bop3<(TA & TB) | (~TA & TC)>(m, a, b); }
 
 // Index of the r-th (0-based) set bit of m (r < popcount(m)).  Binary search over popcounts with
@@ -121,14 +128,14 @@ __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { r
 __device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
   uint32_t sr = ~r;
   uint32_t u = (uint32_t)__popc((uint32_t)m) + sr;
-  uint32_t g = (uint32_t)((int32_t)u >> 31);
+  uint32_t g = sgn(u);
   uint32_t w = msel(g, (uint32_t)(m >> 32), (uint32_t)m);
   sr = msel(g, u, sr);
   uint32_t base = bop3<TA & TB>(g, 32u, 0u);
 #pragma unroll
   for (int k = 16; k >= 1; k >>= 1) {
     u = (uint32_t)__popc(w & ((1u << k) - 1u)) + sr;
-    g = (uint32_t)((int32_t)u >> 31);
+    g = sgn(u);
     if (k > 1) {
       w = msel(g, w >> k, w);
       sr = msel(g, u, sr);
@@ -502,7 +509,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         const uint32_t p = s.ag[i] & XY16;
-        const uint32_t mlive = (uint32_t)((int32_t)((uint32_t)i - n) >> 31);
+        const uint32_t mlive = sgn((uint32_t)i - n);
         atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
       }
       // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
@@ -579,7 +586,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
           for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
           const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
-          const uint32_t mok = (uint32_t)((int32_t)bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u) >> 31);
+          const uint32_t mok = sgn(bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u));
           atomicAnd(&L.occ[p >> 16][tid], bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
           atomicOr(&L.occ[c >> 16][tid], bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
           const uint32_t dxy = c ^ p;
@@ -649,7 +656,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
       for (int j = 0; j < C::R; ++j) {
         if (__any(j < kreq)) {                  // wave-uniform: skip items no env needs
-          uint32_t ma = (uint32_t)((int32_t)((uint32_t)j - (uint32_t)kreq) >> 31);   // j < kreq
+          uint32_t ma = sgn((uint32_t)j - (uint32_t)kreq);   // j < kreq
           uint32_t sel, tgi;
           if (regen) {
             const uint32_t rpos = (uint32_t)regen[e * 2 * C::R + j];
