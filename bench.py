@@ -423,7 +423,7 @@ def main():
             "sampler_path": sampler,
             "policy_path": policy_line,
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # reported at N=1 only
             procs = args.cpu_procs or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(args.variant, NA, procs, args.cpu_seconds)
             out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -201,6 +201,9 @@ struct Regs {
   uint32_t hdr, epi;
   uint32_t ag[C::NAM];
   uint64_t am;   // open requests (bit j = pickup point j has one; kept in registers across steps)
+  // Wave-uniform first step of the expiry phase: W, since a request opened at t0 >= 0 lives W
+  // steps, or 0 if some lane was loaded holding one that expires sooner (no episode reaches that).
+  uint32_t wskip;
 };
 
 template <class C>
@@ -265,7 +268,7 @@ __device__ __forceinline__ uint64_t low_mask() {
 
 template <class C>
 __device__ __forceinline__ void load_env(Regs<C>& s, Lds<C>& L, const uint32_t* __restrict__ st, int64_t B,
-                                         int64_t e, int na, int tid) {
+                                         int64_t e, int na, uint32_t W, int tid) {
   s.hdr = st[e];
   s.epi = st[B + e];
 #pragma unroll
@@ -280,6 +283,16 @@ __device__ __forceinline__ void load_env(Regs<C>& s, Lds<C>& L, const uint32_t* 
   for (int j = 0; j < C::P; ++j)
     L.pkp[j][tid] = (uint16_t)(((pt[j >> 2] >> (8 * (j & 3))) & 0xFFu) | (((pm[j >> 2] >> (8 * (j & 3))) & 0xFFu) << 8));
   s.am = active_mask<C>(pt);
+  // expiry step of each open request: t + (expiry byte - t) mod 256, as the expiry phase counts
+  const uint32_t t0 = s.hdr & 0xFFFFu;
+  bool early = false;
+#pragma unroll
+  for (int j = 0; j < C::P; ++j) {
+    const uint32_t sh = 8 * (j & 3);
+    const uint32_t rem = (((pm[j >> 2] >> sh) & 0xFFu) - t0) & 0xFFu;
+    early |= ((pt[j >> 2] >> sh) & 0xFFu) != 0u && t0 + rem < W;
+  }
+  s.wskip = __any(early) ? 0u : W;
 }
 
 template <class C>
@@ -474,13 +487,14 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 
     // ---- request expiry (core.py:303-306), 4 pickup points per op.  Timer bytes hold the low 8
     //      bits of the step at which the request expires (opened at t0 with wait W: t0 + W, the
-    //      step whose decrement would reach 0), so nothing is decremented; a request opened at
+    //      step whose decrement would reach 0), so nothing is decremented.  A request opened at
     //      t0 >= 0 cannot expire before step W, so waves with every t < W skip the phase (with
-    //      T = W, 199 of 200 steps).  Run before the move: expiry reads no positions and the move
-    //      reads no requests, so the two commute, and the pickup table is final before the move
-    //      loop -- which lets its lookups be issued inside it.
+    //      T = W, 199 of 200 steps) unless they were loaded from a state outside that invariant
+    //      (s.wskip).  Run before the move: expiry reads no positions and the move reads no
+    //      requests, so the two commute, and the pickup table is final before the move loop --
+    //      which lets its lookups be issued inside it.
     asm volatile("; PHASE expire" ::: "memory");
-    if (!(ablate & 4) && __any(t >= W)) {
+    if (!(ablate & 4) && __any(t >= s.wskip)) {
       uint64_t expired = 0;
 #pragma unroll
       for (int j = 0; j < C::P; ++j) {
@@ -897,7 +911,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const Keys k{a.k0, a.k1};
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
-  load_env<C>(s, L, a.state, a.B, e, a.na, tid);
+  load_env<C>(s, L, a.state, a.B, e, a.na, (uint32_t)a.W, tid);
   // Drain the state loads here.  Their first uses are inside the step loop, so otherwise the
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).

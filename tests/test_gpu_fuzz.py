@@ -23,7 +23,7 @@ def wh():
     return warehouse
 
 
-def random_states(L, B, nmax, rng):
+def random_states(L, B, nmax, rng, ts=None):
     P, Dp, R, W, D = L.P, L.Dp, L.R, L.W, L.D
     pk, dl, _, _ = ob.tables(L)
     n = rng.randint(1, nmax + 1, size=B)
@@ -31,7 +31,7 @@ def random_states(L, B, nmax, rng):
     atg = np.full((B, nmax), -1, np.int32)
     tgt = np.full((B, P), -1, np.int32)
     tim = np.full((B, P), -1, np.int32)
-    t = rng.choice([0, 5, L.T - 1, L.T, 150], size=B).astype(np.int64)
+    t = rng.choice(ts if ts is not None else [0, 5, L.T - 1, L.T, 150], size=B).astype(np.int64)
     for e in range(B):
         k = n[e]
         mode = rng.randint(4)
@@ -59,14 +59,11 @@ def random_states(L, B, nmax, rng):
     return n.astype(np.int32), pos, atg, tgt, tim, t
 
 
-@pytest.mark.parametrize("variant", ["small", "medium", "large"])
-@pytest.mark.parametrize("ordered", [False, True])
-def test_fuzz_single_transitions(wh, variant, ordered):
+def run_fuzz(wh, variant, ordered, seed, ts=None, B=3000):
     L = oc.layout_for(variant)
     nmax = oc.VARIANTS[variant]["nmax"]
-    B = 3000
-    rng = np.random.RandomState(100 + nmax + (7 if ordered else 0))
-    n, pos, atg, tgt, tim, t = random_states(L, B, nmax, rng)
+    rng = np.random.RandomState(seed)
+    n, pos, atg, tgt, tim, t = random_states(L, B, nmax, rng, ts)
     env = wh.BatchedWarehouse(variant, B, train=True)
     env.from_canonical(dict(pos=pos, agent_target=atg, pickup_target=tgt, pickup_timer=tim, t=t, n=n))
     S = ob.BState(pos=pos.copy(), agent_tgt=atg.copy(), pk_tgt=tgt.copy(), pk_timer=tim.copy(), t=t.copy(),
@@ -99,3 +96,18 @@ def test_fuzz_single_transitions(wh, variant, ordered):
     np.testing.assert_array_equal(rew.cpu().numpy(), orew)
     np.testing.assert_array_equal(done.cpu().numpy().astype(bool), odone)
     np.testing.assert_array_equal(env.observe().cpu().numpy(), ob.observe(L, S))
+
+
+@pytest.mark.parametrize("variant", ["small", "medium", "large"])
+@pytest.mark.parametrize("ordered", [False, True])
+def test_fuzz_single_transitions(wh, variant, ordered):
+    nmax = oc.VARIANTS[variant]["nmax"]
+    run_fuzz(wh, variant, ordered, 100 + nmax + (7 if ordered else 0))
+
+
+@pytest.mark.parametrize("variant", ["small", "medium", "large"])
+def test_fuzz_expiry_far_below_w(wh, variant):
+    """Whole waves at t < W holding requests about to expire (states no episode reaches: a request
+    opened at t0 >= 0 lives W steps).  The kernel must not assume reachability to skip expiry."""
+    nmax = oc.VARIANTS[variant]["nmax"]
+    run_fuzz(wh, variant, False, 300 + nmax, ts=[0, 5, 150])
