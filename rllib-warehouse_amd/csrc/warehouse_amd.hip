@@ -196,6 +196,13 @@ __device__ __forceinline__ uint32_t action_of(uint32_t d) {
   return (uint32_t)(3 * ((int)v.x + 1) + ((int)v.y + 1));
 }
 
+// Phase labels in the device assembly for instruction-count analysis; -DWH_NO_PHASE_MARKS drops them.
+#ifndef WH_NO_PHASE_MARKS
+#define WH_PHASE_MARK(name) asm volatile("; PHASE " #name ::: "memory")
+#else
+#define WH_PHASE_MARK(name) ((void)0)
+#endif
+
 template <class C>
 struct Regs {
   uint32_t hdr, epi;
@@ -407,7 +414,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       }
     }
   } else {
-    asm volatile("; PHASE policy_rtag" ::: "memory");
+    WH_PHASE_MARK(policy_rtag);
     // Open requests in ascending pickup order (core.py:409-418).  Index P of the tables is a
     // sentinel (far-away cell, null-cell tag) that fills missing slots; after a reset every slot is
     // the sentinel, so every agent's "nearest request" is the null cell, which is where the
@@ -430,7 +437,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       mlo = (uint32_t)m;
       mhi = (uint32_t)(m >> 32);
     }
-    asm volatile("; PHASE policy_agents" ::: "memory");
+    WH_PHASE_MARK(policy_agents);
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i) {
       const uint32_t a = s.ag[i];
@@ -493,7 +500,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     //      (s.wskip).  Run before the move: expiry reads no positions and the move reads no
     //      requests, so the two commute, and the pickup table is final before the move loop --
     //      which lets its lookups be issued inside it.
-    asm volatile("; PHASE expire" ::: "memory");
+    WH_PHASE_MARK(expire);
     if (!(ablate & 4) && __any(t >= s.wskip)) {
       uint64_t expired = 0;
 #pragma unroll
@@ -507,7 +514,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     }
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
-    asm volatile("; PHASE move" ::: "memory");
+    WH_PHASE_MARK(move);
     uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329): cell_row,
                                                     // target byte, delivery cell
     bool looked = false;
@@ -622,7 +629,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 
     // ---- pickups: every agent decided against the pre-pickup table, then the table is cleared
     //      (core.py:309-335; two agents on one point both pick it up)
-    asm volatile("; PHASE pickup" ::: "memory");
+    WH_PHASE_MARK(pickup);
     if (!(ablate & 8)) {
       if (!looked) {
 #pragma unroll
@@ -652,7 +659,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   }
 
   // ---- regeneration: reopen k = R - P + |inactive| points (core.py:338-351)
-  asm volatile("; PHASE regen" ::: "memory");
+  WH_PHASE_MARK(regen);
   if (!(ablate & 16)) {
     const uint64_t inactive = ~s.am & low_mask<C::P>();
     const uint32_t nin = (uint32_t)__popcll(inactive);
@@ -708,7 +715,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   bool done = false;
   if (phase != PH_REGEN) {
     // ---- deliveries (core.py:354-368): target cell == position (idle agents never match)
-    asm volatile("; PHASE deliver" ::: "memory");
+    WH_PHASE_MARK(deliver);
     if (!(ablate & 32)) {
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
@@ -720,7 +727,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     }
 #pragma unroll
     for (int i = 0; i < C::NAM; ++i) rew[i] = __uint_as_float(bop3<TA & TB>(rewm[i], 0x3F800000u, 0u));
-    asm volatile("; PHASE tail" ::: "memory");
+    WH_PHASE_MARK(tail);
     done = t >= T;                                            // core.py:438
     s.hdr = t | (n << 16);                                    // clears `fresh`
   }

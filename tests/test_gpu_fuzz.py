@@ -23,7 +23,7 @@ def wh():
     return warehouse
 
 
-def random_states(L, B, nmax, rng, ts=None):
+def random_states(L, B, nmax, rng, ts=None, full=False):
     P, Dp, R, W, D = L.P, L.Dp, L.R, L.W, L.D
     pk, dl, _, _ = ob.tables(L)
     n = rng.randint(1, nmax + 1, size=B)
@@ -47,7 +47,7 @@ def random_states(L, B, nmax, rng, ts=None):
         else:
             p = rng.randint(0, D, size=(k, 2))
         pos[e, :k] = np.clip(p, 0, D - 1)
-        na = rng.randint(max(0, R - k), R + 1)
+        na = R if full else rng.randint(max(0, R - k), R + 1)
         sel = rng.choice(P, na, replace=False)
         tgt[e, sel] = rng.randint(0, Dp, na)
         tim[e, sel] = np.where(rng.rand(na) < 0.3, 1, rng.randint(1, W + 1, na))
@@ -111,3 +111,38 @@ def test_fuzz_expiry_far_below_w(wh, variant):
     opened at t0 >= 0 lives W steps).  The kernel must not assume reachability to skip expiry."""
     nmax = oc.VARIANTS[variant]["nmax"]
     run_fuzz(wh, variant, False, 300 + nmax, ts=[0, 5, 150])
+
+
+@pytest.mark.parametrize("variant", ["small", "medium", "large"])
+def test_fused_rollout_from_fuzzed_states(wh, variant):
+    """wh_rollout (greedy, philox regeneration and auto-reset, K steps in one launch) started from
+    fuzzed states -- t far below W with requests about to expire, crowded agents, t at T-1 -- against
+    the oracle stepping the same philox contract.  Every state holds R open requests, as every
+    reachable pre-step state does (the solver reads exactly R request rows, solvers.py:53-58)."""
+    import torch
+
+    L = oc.layout_for(variant)
+    nmax = oc.VARIANTS[variant]["nmax"]
+    B, K, seed = 2048, 40, 11
+    rng = np.random.RandomState(500 + nmax)
+    n, pos, atg, tgt, tim, t = random_states(L, B, nmax, rng, ts=[0, 5, 150, L.T - 1], full=True)
+    env = wh.BatchedWarehouse(variant, B, train=True, seed=seed)
+    env.from_canonical(dict(pos=pos, agent_target=atg, pickup_target=tgt, pickup_timer=tim, t=t, n=n))
+    S = ob.BState(pos=pos.copy(), agent_tgt=atg.copy(), pk_tgt=tgt.copy(), pk_timer=tim.copy(), t=t.copy(),
+                  n=n.copy(), fresh=np.zeros(B, bool), episode=np.zeros(B, np.uint32))
+    rew = torch.zeros((K, B, nmax), device=env.device)
+    dn = torch.zeros((K, B), dtype=torch.uint8, device=env.device)
+    env.rollout(K, "greedy", 0.0, rewards=rew, dones=dn)
+    d = ob.PhiloxDraws(seed, np.arange(B))
+    for s in range(K):
+        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        np.testing.assert_array_equal(rew[s].cpu().numpy(), orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
+    c = {k: v.cpu().numpy() for k, v in env.to_canonical().items()}
+    np.testing.assert_array_equal(c["pos"], S.pos)
+    np.testing.assert_array_equal(c["agent_target"], S.agent_tgt)
+    np.testing.assert_array_equal(c["pickup_target"], S.pk_tgt)
+    np.testing.assert_array_equal(c["pickup_timer"], S.pk_timer)
+    np.testing.assert_array_equal(c["t"], S.t)
