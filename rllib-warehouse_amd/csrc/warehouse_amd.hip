@@ -131,18 +131,17 @@ __device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
   uint32_t g = sgn(u);
   uint32_t w = msel(g, (uint32_t)(m >> 32), (uint32_t)m);
   sr = msel(g, u, sr);
-  uint32_t base = bop3<TA & TB>(g, 32u, 0u);
+  const uint32_t half = bop3<TA & TB>(g, 32u, 0u);
+  // binary search inside w: the field of width k at offset base (v_bfe) instead of shifting w
+  uint32_t base = 0;
 #pragma unroll
   for (int k = 16; k >= 1; k >>= 1) {
-    u = (uint32_t)__popc(w & ((1u << k) - 1u)) + sr;
+    u = (uint32_t)__popc(__builtin_amdgcn_ubfe(w, base, (uint32_t)k)) + sr;
     g = sgn(u);
-    if (k > 1) {
-      w = msel(g, w >> k, w);
-      sr = msel(g, u, sr);
-    }
+    if (k > 1) sr = msel(g, u, sr);
     base = bop3<(TA & TB) | TC>(g, (uint32_t)k, base);
   }
-  return base;
+  return base | half;
 }
 
 // high bit of every nonzero byte
