@@ -46,7 +46,7 @@ constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 struct TableLayout {
   int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
-      : cell(0), rp(512 * D), tag(512 * D + 4 * (P + 1)), dst(512 * D + 8 * (P + 1)),
+      : cell(0), rp(512 * D), tag(512 * D + 4), dst(512 * D + 8 * (P + 1)),   // rp/tag interleaved
         mv(512 * D + 8 * (P + 1) + 4 * DP), valid(512 * D + 8 * (P + 1) + 4 * DP + 48),
         bytes(512 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
@@ -214,7 +214,7 @@ struct Regs {
 
 template <class C>
 struct Lds {
-  uint32_t tbl[C::TBLW];
+  alignas(16) uint32_t tbl[C::TBLW];
   uint32_t occ[C::D][BT];        // occupancy row y: bit x
   // Pickup point j of lane tid: low byte = request target + 1 (0 = none), high byte = expiry step
   // (low 8 bits).  Row P is scratch: predicated stores of lanes with nothing to write go there.
@@ -229,8 +229,10 @@ struct Lds {
     return reinterpret_cast<const uint16_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
   }
 
-  __device__ __forceinline__ uint32_t rp(uint32_t j) const { return tbl[C::T.rp / 4 + j]; }
-  __device__ __forceinline__ uint32_t tag(uint32_t j) const { return tbl[C::T.tag / 4 + j]; }
+  // (pickup cell, greedy tag) of point j: one 8-byte LDS read
+  __device__ __forceinline__ uint2 rtag(uint32_t j) const {
+    return reinterpret_cast<const uint2*>(&tbl[C::T.rp / 4])[j];
+  }
   __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
   __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
   __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
@@ -429,8 +431,9 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       asm("v_ffbl_b32 %0, %1" : "=v"(fhi) : "v"(mhi));
       const uint32_t j = __builtin_elementwise_min(
           __builtin_elementwise_min(flo, __builtin_elementwise_add_sat(fhi, 32u)), (uint32_t)C::P);
-      rp[r] = L.rp(j);
-      tg[r] = L.tag(j);
+      const uint2 v = L.rtag(j);
+      rp[r] = v.x;
+      tg[r] = v.y;
       uint64_t m = ((uint64_t)mhi << 32) | mlo;
       m &= m - 1ull;
       mlo = (uint32_t)m;
@@ -1049,7 +1052,7 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   const int tid = threadIdx.x;
   const uint32_t* srcg = &kObsSrc<C::R, C::NAM>.w[0][0];
   for (int k = tid; k < 2 * SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
-  for (int k = tid; k < C::P; k += BT) O.rp[k] = tables[C::T.rp / 4 + k];
+  for (int k = tid; k < C::P; k += BT) O.rp[k] = tables[C::T.rp / 4 + 2 * k];
   for (int k = tid; k < C::DP; k += BT) O.dst[k] = tables[C::T.dst / 4 + k];
 
   const int64_t e0 = (int64_t)blockIdx.x * OBS_EB;
@@ -1261,9 +1264,10 @@ int validate(const wh_config* c, Geometry* g) {
 
 // Host copy of the per-workgroup tables, same layout as TableLayout (core.py:170-199):
 //   cell  [256*D] u16: (x | y << 8) -> (pickup index + 1) * ROWB, 0 = not a pickup cell
-//   rp    [P+1]  u32 : pickup cell as x | y << 16; [P] = far-away cell (never nearest)
-//   tag   [P+1]  u32 : pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58);
-//                      [P] = the null cell (D/2, D/2): where fresh-reset agents head (core.py:233-236)
+//   rp/tag [P+1] u32 pairs, interleaved (the policy reads both with one 8-byte LDS read):
+//          rp  = pickup cell as x | y << 16; [P] = far-away cell (never nearest)
+//          tag = pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58);
+//                [P] = the null cell (D/2, D/2): where fresh-reset agents head (core.py:233-236)
 //   dst   [Dp]   u32 : delivery cell as x | y << 16
 //   mv    [12]   u32 : MOVES[a] as packed i16 (dx, dy) (core.py:38)
 //   valid [NV]   u32 : interior non-pickup cells x | y << 16, ascending (x, y) (spawn, core.py:191-199)
@@ -1304,8 +1308,10 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
       if (!cell[x | (y << 8)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
   std::vector<uint32_t> words(cell.size() / 2, 0);
   memcpy(words.data(), cell.data(), cell.size() * 2);
-  words.insert(words.end(), rp.begin(), rp.end());
-  words.insert(words.end(), tag.begin(), tag.end());
+  for (int j = 0; j <= g.P; ++j) {
+    words.push_back(rp[j]);
+    words.push_back(tag[j]);
+  }
   words.insert(words.end(), dst.begin(), dst.end());
   words.insert(words.end(), mv.begin(), mv.end());
   words.insert(words.end(), valid.begin(), valid.end());
