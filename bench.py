@@ -69,7 +69,27 @@ def cpu_worker(args):
     return steps * n, spent
 
 
-def cpu_baseline(variant, n, procs, seconds):
+def host_cores():
+    """Host cores this job may use: os.cpu_count(), narrowed by the CPU affinity mask and by a
+    cgroup v2 CPU quota (a GPU box shares a large host, so os.cpu_count() alone over-counts).
+    Returns (cores, detail)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(c for c in (total, aff, quota) if c)
+    return cores, f"os.cpu_count()={total}, affinity={aff}, cgroup quota={quota or 'none'}"
+
+
+def cpu_baseline(variant, n, procs, seconds, detail=""):
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -77,20 +97,36 @@ def cpu_baseline(variant, n, procs, seconds):
         res = pool.map(cpu_worker, [(variant, n, seconds, 1000 + i) for i in range(procs)])
     rate = sum(a / s for a, s in res if s > 0)
     return dict(value=rate, unit="agent-steps/s", cores=procs, kind="port",
-                sample=f"{procs} processes x {seconds:.1f} s, 1 env each, {variant} N={n}, greedy actions, "
-                       f"step-only time of oracle/core.py OracleWarehouse.step (numpy restatement of "
-                       f"warehouse.core.Warehouse.step)")
+                sample=f"one process per host core ({procs}; {detail}) x {seconds:.1f} s, 1 env each, "
+                       f"{variant} N={n}, greedy actions, step-only time of oracle/core.py "
+                       f"OracleWarehouse.step (numpy restatement of warehouse.core.Warehouse.step)")
 
 
-def load_traffic(tag):
+def source_sha():
+    """sha256 of the kernel sources: profile-derived fields are reported only when the committed
+    profile was taken from the same sources."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "rllib-warehouse_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def load_profile(tag):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
     try:
-        d = json.load(open(path))
-        return d.get(tag, {}).get("bytes_per_launch")
+        d = json.load(open(path))[tag]
     except Exception:
         return None
+    return d if d.get("source_sha") == source_sha() else None
+
+
+def load_traffic(tag, launches_bytes=None):
+    d = load_profile(tag)
+    return None if d is None else d.get("bytes_per_launch")
 
 
 def config_name(variant, na, envs, policy):
@@ -101,34 +137,95 @@ def config_name(variant, na, envs, policy):
 
 
 def load_issue(tag, steps_per_launch):
-    """VALU issue view of the step kernel from the committed SQ counters (tools/profile_round.sh
-    with SQ=1 -> profiles/pmc_traffic.json): per wave and env-step, VALU instructions and wave
-    quad-cycles; one wave issues at most one VALU per quad-cycle (MI355X_MICROARCH.md)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """VALU issue view of the step kernel from the committed SQ counters (profiles/pmc_traffic.json,
+    same kernel sources only): per wave and env-step, VALU instructions and wave quad-cycles; one
+    wave alone issues at most one VALU per quad-cycle (MI355X_MICROARCH.md)."""
+    d = load_profile(tag)
     try:
-        sq = json.load(open(path))[tag]["sq"]
+        sq = d["sq"]
+        spl = d.get("steps_per_launch", steps_per_launch)
         waves = sq["SQ_WAVES"]
-        valu = sq["SQ_INSTS_VALU"] / waves / steps_per_launch
-        cyc = sq["SQ_WAVE_CYCLES"] / waves / steps_per_launch
+        valu = sq["SQ_INSTS_VALU"] / waves / spl
+        cyc = sq["SQ_WAVE_CYCLES"] / waves / spl
         return {"valu_per_wave_step": valu, "wave_quad_cycles_per_step": cyc, "valu_issue_frac": valu / cyc,
-                "lds_per_wave_step": sq["SQ_INSTS_LDS"] / waves / steps_per_launch,
-                "source": f"profiles/pmc_traffic.json:{tag}.sq"}
+                "lds_per_wave_step": sq["SQ_INSTS_LDS"] / waves / spl,
+                "source": f"profiles/pmc_traffic.json:{tag}.sq ({spl} steps per launch)"}
     except Exception:
         return None
 
 
+# ----------------------------------------------------------------------------- multi-GPU plumbing
+def rank_info(environ=None):
+    """(world, rank, local_rank) from the torch.distributed.run environment (1, 0, 0 without it)."""
+    env = os.environ if environ is None else environ
+    return int(env.get("WORLD_SIZE", "1")), int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+
+
+def shard_offset(rank, envs_per_gpu):
+    """Rank r owns global env ids [r*B, (r+1)*B): philox draws are keyed by global id, so the shards
+    together run exactly the trajectories of one batch of world*B envs (no collective needed)."""
+    return rank * envs_per_gpu
+
+
+def timed_window(run, sync, world, dist):
+    """The contract's timing window: barrier + device sync on both sides of `run`, then the MAX of
+    the per-rank elapsed times (gloo; nothing on the data path).  Returns seconds."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def aggregate_rate(world, envs_per_gpu, agents, steps, elapsed):
+    """Whole-job agent-steps/s: every rank stepped its B envs x agents for `steps` steps inside the
+    window whose length is the slowest rank's."""
+    return world * envs_per_gpu * agents * steps / elapsed
+
+
+def window_setup_steps(T, K, W):
+    """Untimed steps before the warmup so that the timed window [s+W, s+W+K) is centred on an
+    episode end (t = T: done, auto-reset, and the expiry of the reset-time requests, core.py:303-306,
+    438): s + W + K//2 = T (mod T)."""
+    return (T - (K // 2) % T - W) % T
+
+
+def launch_plan(K, chunk):
+    """Steps per fused launch covering K steps."""
+    plan = [chunk] * (K // chunk)
+    if K % chunk:
+        plan.append(K % chunk)
+    return plan
+
+
 def measure(env, mode, policy, K, W, chunk, dev, world, dist):
-    """Time K steps of `mode`; returns (elapsed_s_max_over_ranks, kernel_ms, steps_per_launch)."""
+    """Time K steps of `mode` (the contract's window).  The kernel time comes from HIP events recorded
+    on the launch stream INSIDE that window around exactly the timed launches, so the roofline
+    describes the launches that were timed.  Returns a dict."""
     import torch
 
     B, NA = env.B, env.agent_slots
+    T = int(env.geometry["T"])
     stream = torch.cuda.current_stream(dev)
+    setup = window_setup_steps(T, K, W)
+    if setup:
+        env.rollout(setup, policy, 0.0)           # position the window (untimed, no outputs)
+    whole = K * B * (NA * 4 + 1) <= (4 << 30)     # per-step outputs of the whole window fit: keep them all
     if mode == "graph":
-        rew = torch.zeros((1, B, NA), device=dev)
-        dn = torch.zeros((1, B), dtype=torch.uint8, device=dev)
-
-        def one():
-            env.rollout(1, policy, 0.0, rewards=rew, dones=dn)
+        rew1 = torch.zeros((1, B, NA), device=dev)
+        dn1 = torch.zeros((1, B), dtype=torch.uint8, device=dev)
+        def one():   # reads the current stream per call: the capture runs on a side stream
+            env.rollout(1, policy, 0.0, rewards=rew1, dones=dn1)
 
         for _ in range(max(W, 3)):
             one()
@@ -138,57 +235,49 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist):
         with torch.cuda.graph(graph):
             for _ in range(G):
                 one()
+        # capture replays nothing: the G captured steps run only in the timed window
         torch.cuda.synchronize(dev)
-
-        def run_steps(k):
-            for _ in range(k // G):
-                graph.replay()
-            for _ in range(k % G):
-                one()
-
-        def timed_unit():
-            graph.replay()
-        per_unit_launches, spl = G, 1
+        tail = env.rollout_launcher(1, policy, 0.0, rewards=rew1, dones=dn1)
+        launches = [graph.replay] * (K // G) + [tail] * (K % G)
+        plan = [1] * K
+        dn = None
     else:
-        C = chunk
-        rew = torch.zeros((C, B, NA), device=dev)
-        dn = torch.zeros((C, B), dtype=torch.uint8, device=dev)
+        plan = launch_plan(K, chunk)
+        if whole:
+            rew = torch.zeros((K, B, NA), device=dev)
+            dn = torch.zeros((K, B), dtype=torch.uint8, device=dev)
+        else:
+            rew = torch.zeros((chunk, B, NA), device=dev)
+            dn = torch.zeros((chunk, B), dtype=torch.uint8, device=dev)
+        launches, off = [], 0
+        for c in plan:
+            o = off if whole else 0
+            launches.append(env.rollout_launcher(c, policy, 0.0, rewards=rew[o:o + c], dones=dn[o:o + c]))
+            off += c
+        if W:
+            wr = torch.zeros((min(W, chunk), B, NA), device=dev)
+            wd = torch.zeros((min(W, chunk), B), dtype=torch.uint8, device=dev)
+            for c in launch_plan(W, chunk):
+                env.rollout(c, policy, 0.0, rewards=wr[:c], dones=wd[:c])
+            del wr, wd
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-        def run_steps(k):
-            while k > 0:
-                c = min(C, k)
-                env.rollout(c, policy, 0.0, rewards=rew[:c], dones=dn[:c])
-                k -= c
-        run_steps(max(W, 1))
+    def run():
+        ev0.record(stream)
+        for launch in launches:
+            launch()
+        ev1.record(stream)
 
-        def timed_unit():
-            env.rollout(C, policy, 0.0, rewards=rew, dones=dn)
-        per_unit_launches, spl = 1, C
-
-    # ---------------- timed region: barrier + sync on both sides, max over ranks
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(K)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # ---------------- kernel duration: HIP events on the launch stream around back-to-back
-    # launches (a graph replay of G one-step launches, or one fused launch), median of 7
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(7)]
-    for a, b in evs:
-        a.record(stream)
-        timed_unit()
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    kms = sorted(a.elapsed_time(b) / per_unit_launches for a, b in evs)
-    return elapsed, kms[len(kms) // 2], spl
+    elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
+    span_ms = ev0.elapsed_time(ev1)
+    kernels = len(plan)
+    bytes_total = sum(B * (2 * 4 * env.layout.words_per_env + c * (4 * NA + 1)) for c in plan)
+    dones = int(dn.sum().item()) if (dn is not None and whole) else None
+    return dict(elapsed=elapsed, span_ms=span_ms, kernel_ms=span_ms / kernels, launches=kernels,
+                steps_per_launch=plan[0], bytes_per_launch=bytes_total / kernels,
+                achieved_gbs=bytes_total / (span_ms * 1e-3) / 1e9, bytes_per_env_step=bytes_total / (B * K),
+                host_fixed_us=(elapsed * 1e3 - span_ms) * 1e3, setup_steps=setup,
+                window_t=[(setup + W) % T, (setup + W + K) % T], dones_in_window=dones)
 
 
 def measure_sampler(env, K, W, dev, world, dist):
@@ -211,21 +300,14 @@ def measure_sampler(env, K, W, dev, world, dist):
         for _ in range(G):
             one()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(K // G):
-        graph.replay()
-    for _ in range(K % G):
-        one()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    def run():
+        for _ in range(K // G):
+            graph.replay()
+        for _ in range(K % G):
+            one()
+
+    elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
     # observe kernel alone: 20 back-to-back launches between HIP events on the launch stream
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
     for a, b in evs:
@@ -265,21 +347,14 @@ def measure_policy(env, K, W, dev, world, dist):
         for _ in range(G):
             one()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(K // G):
-        graph.replay()
-    for _ in range(K % G):
-        one()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    def run():
+        for _ in range(K // G):
+            graph.replay()
+        for _ in range(K % G):
+            one()
+
+    elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
     for a, b in evs:
         a.record(stream)
@@ -289,6 +364,35 @@ def measure_policy(env, K, W, dev, world, dist):
     torch.cuda.synchronize(dev)
     kms = sorted(a.elapsed_time(b) / 5 for a, b in evs)
     return elapsed, kms[len(kms) // 2], net
+
+
+def step_roofline(m, variant, NA, policy, mode):
+    """The bench line's `roofline` for the timed launches of measure() (dict m)."""
+    tag = f"{variant}_n{NA}_{mode}_k{m['steps_per_launch']}"
+    prof = load_profile(tag)
+    return {
+        "bound": "hbm",
+        "achieved": m["achieved_gbs"],
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": m["achieved_gbs"] / HBM_PEAK_GBS,
+        "traffic": None if prof is None else prof.get("bytes_per_launch"),
+        "kernel": f"k_step<Cfg<D,R,racks,{NA}>, {policy}>",
+        "kernel_ms": m["kernel_ms"],
+        "launches": m["launches"],
+        "steps_per_launch": m["steps_per_launch"],
+        "bytes_per_launch": m["bytes_per_launch"],
+        "bytes_per_env_step": m["bytes_per_env_step"],
+        "host_fixed_us": m["host_fixed_us"],
+        "rocprof_avg_ms": None if prof is None or prof.get("avg_ns") is None else prof["avg_ns"] * 1e-6,
+        "issue": load_issue(tag, m["steps_per_launch"]),
+        "profile": None if prof is None else f"profiles/pmc_traffic.json:{tag}",
+        "note": "kernel_ms = HIP-event span of the timed launches / launches (events on the launch "
+                "stream inside the timed window); host_fixed_us = window wall time - that span "
+                "(launch + completion latency); algorithmic bytes = 2 x packed state + per-step "
+                "rewards/dones; the kernel keeps state in registers and is VALU-issue bound "
+                "(DESIGN.md §5)",
+    }
 
 
 def main():
@@ -308,7 +412,7 @@ def main():
     ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
     ap.add_argument("--no-policy", action="store_true", help="skip the SAC-policy rollout measurement")
     ap.add_argument("--policy-steps", type=int, default=200)
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = one per host core (host_cores())")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -316,36 +420,32 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_info()
+    torch.cuda.set_device(local)             # before any other GPU call of this rank
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     import warehouse
 
     B, NA, K, W = args.envs, args.agents, args.steps, args.warmup
-    env = warehouse.BatchedWarehouse(args.variant, B, NA, seed=1234, env_offset=rank * B, device=dev)
+    env = warehouse.BatchedWarehouse(args.variant, B, NA, seed=1234, env_offset=shard_offset(rank, B), device=dev)
     env.reset()
-    words = env.layout.words_per_env
-    out_b = 4 * NA + 1                       # rewards f32 x NA + done u8, per env-step
 
-    elapsed, kernel_ms, spl = measure(env, args.mode, args.policy, K, W, args.chunk, dev, world, dist)
-    value = world * B * NA * K / elapsed
-    bytes_per_launch = B * (2 * 4 * words + spl * out_b)
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    m = measure(env, args.mode, args.policy, K, W, args.chunk, dev, world, dist)
+    value = aggregate_rate(world, B, NA, K, m["elapsed"])
     alt = None
     if not args.no_alt:
         other = "graph" if args.mode == "fused" else "fused"
-        el2, kms2, spl2 = measure(env, other, args.policy, K, W, args.chunk, dev, world, dist)
-        bpl2 = B * (2 * 4 * words + spl2 * out_b)
-        alt = {"mode": other, "value": world * B * NA * K / el2, "ms_per_step": el2 * 1e3 / K,
-               "kernel_ms": kms2, "steps_per_launch": spl2, "bytes_per_launch": bpl2,
-               "roofline_frac": bpl2 / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-               "traffic": load_traffic(f"{args.variant}_n{NA}_{other}")}
+        env.reset()
+        m2 = measure(env, other, args.policy, K, W, args.chunk, dev, world, dist)
+        alt = {"mode": other, "value": aggregate_rate(world, B, NA, K, m2["elapsed"]),
+               "ms_per_step": m2["elapsed"] * 1e3 / K, "kernel_ms": m2["kernel_ms"],
+               "steps_per_launch": m2["steps_per_launch"], "bytes_per_launch": m2["bytes_per_launch"],
+               "roofline_frac": m2["achieved_gbs"] / HBM_PEAK_GBS, "host_fixed_us": m2["host_fixed_us"],
+               "traffic": load_traffic(f"{args.variant}_n{NA}_{other}_k{m2['steps_per_launch']}")}
 
+    words = env.layout.words_per_env
     sampler = None
     if not args.no_sampler:
         Ks = min(K, 1000)
@@ -354,7 +454,7 @@ def main():
         sampler = {
             "workload": f"RLlib sampler route: device greedy actions -> wh_vector_step (step + auto-reset "
                         f"+ f32 observation rows [B,{NA},{env.obs_len}]), hipGraph of 100 steps",
-            "value": world * B * NA * Ks / el3, "unit": "agent-steps/s", "steps": Ks,
+            "value": aggregate_rate(world, B, NA, Ks, el3), "unit": "agent-steps/s", "steps": Ks,
             "ms_per_step": el3 * 1e3 / Ks,
             "roofline": {"bound": "hbm", "kernel": "k_observe", "kernel_ms": oms,
                          "bytes_per_launch": obs_b, "achieved": obs_b / (oms * 1e-3) / 1e9,
@@ -373,8 +473,8 @@ def main():
             "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
                         f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset + "
                         f"observation rows); random-init weights (no checkpoint ships with the reference)",
-            "value": world * B * NA * Kp / el4, "unit": "agent-steps/s", "steps": Kp,
-            "ms_per_step": el4 * 1e3 / Kp, "dtype": "bf16 MFMA, f32 accumulate",
+            "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,
+            "ms_per_step": el4 * 1e3 / Kp, "dtype": f"{getattr(net, 'precision', 'bf16')} MFMA, f32 accumulate",
             "roofline": {"bound": "mfma", "kernel": "k_mlp", "kernel_ms": mms, "flop_per_launch": flop,
                          "achieved": flop / (mms * 1e-3) / 1e12, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": flop / (mms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS,
@@ -389,7 +489,7 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": W,
-            "ms_per_step": elapsed * 1e3 / K,
+            "ms_per_step": m["elapsed"] * 1e3 / K,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -399,33 +499,23 @@ def main():
                 "workload": f"{config_name(args.variant, NA, B, args.policy)}: {args.variant} N={NA}, B={B} envs/GPU, "
                             f"{args.policy} policy fused with step + auto-reset (device-resident rollout)",
                 "envs_per_gpu": B, "agents": NA, "variant": args.variant, "policy": args.policy,
-                "launch": "hipGraph of 1-step launches" if args.mode == "graph" else f"{spl} steps per launch",
+                "launch": "hipGraph of 1-step launches" if args.mode == "graph" else
+                          f"{m['launches']} launch(es) of {m['steps_per_launch']} steps",
                 "parallelism": f"independent env shards x{world}, no collectives",
+                "window": {"setup_steps": m["setup_steps"], "t_at_start_end": m["window_t"],
+                           "dones_in_window": m["dones_in_window"],
+                           "note": "untimed setup steps place the timed window across an episode end "
+                                   "(done + auto-reset + request expiry inside it)"},
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(f"{args.variant}_n{NA}_{args.mode}"),
-                "kernel": f"k_step<Cfg<D,R,racks,{NA}>, {args.policy}>",
-                "kernel_ms": kernel_ms,
-                "steps_per_launch": spl,
-                "bytes_per_launch": bytes_per_launch,
-                "bytes_per_env_step": bytes_per_launch / B / spl,
-                "issue": load_issue(f"{args.variant}_n{NA}_{args.mode}", spl),
-                "note": "algorithmic bytes = 2 x packed state + per-step rewards/dones; the fused kernel "
-                        "keeps state in registers and is VALU-issue bound (one wave per SIMD at B=65536): "
-                        "`issue` is its VALU issue rate against one wave's ceiling (DESIGN.md §5)",
-            },
+            "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,
             "sampler_path": sampler,
             "policy_path": policy_line,
         }
         if not args.no_cpu_baseline and world == 1:   # reported at N=1 only
-            procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(args.variant, NA, procs, args.cpu_seconds)
+            cores, detail = host_cores()
+            procs = args.cpu_procs or cores
+            out["cpu_baseline"] = cpu_baseline(args.variant, NA, procs, args.cpu_seconds, detail)
             out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if world > 1:

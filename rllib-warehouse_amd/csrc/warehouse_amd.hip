@@ -221,7 +221,9 @@ struct Lds {
   // One 16-bit cell per (point, lane) makes every per-point access a single ds op whose address
   // is j * BT + tid, and keeps the pickup table out of the VGPRs.
   uint16_t pkp[C::P + 1][BT];
-  uint32_t agl[C::NAM][BT];      // agent words when processing in action-dict order
+  // Agent words when processing in action-dict order; afterwards the reward-row staging area.
+  // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
+  alignas(16) uint32_t agl[C::NAM][BT];
   // Cell (x | y << 16) -> (pickup index + 1) * ROWB, 0 for other cells: the byte offset of the
   // point's row in pkp, counted from the row before it, so a lookup is one v_perm + one ds_read
   // and the dependent target read one add.
@@ -771,10 +773,13 @@ __device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::N
       if (i < na) row[i] = rew[i];
     return;
   }
-  float* stg = reinterpret_cast<float*>(&L.agl[0][0]) + (tid >> 6) * 64 * C::NAM;
+  // Staging element k of this wave's 64*na floats lives at agl[k / 64][wave base + k % 64]: inside
+  // the wave's own columns, so no other wave's agent words (ordered path) are overwritten.
+  const int wbase = tid & ~63;
+  auto stg = [&](int k) -> float* { return reinterpret_cast<float*>(&L.agl[k >> 6][wbase + (k & 63)]); };
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i)
-    if (i < na) stg[lane * na + i] = rew[i];
+    if (i < na) *stg(lane * na + i) = rew[i];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -783,12 +788,12 @@ __device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::N
   if ((reinterpret_cast<uintptr_t>(wout) & 15u) == 0 && (na & 3) == 0) {
 #pragma unroll
     for (int q = 0; q < C::NAM / 4; ++q)
-      if (4 * q < na)
-        reinterpret_cast<float4*>(wout)[lane + 64 * q] = reinterpret_cast<const float4*>(stg)[lane + 64 * q];
+      if (4 * q < na)   // 4 consecutive k (k % 4 == 0) sit in one row, 16-byte aligned
+        reinterpret_cast<float4*>(wout)[lane + 64 * q] = *reinterpret_cast<const float4*>(stg(4 * (lane + 64 * q)));
   } else {
 #pragma unroll
     for (int q = 0; q < C::NAM; ++q)
-      if (lane + 64 * q < nvalid) wout[lane + 64 * q] = stg[lane + 64 * q];
+      if (lane + 64 * q < nvalid) wout[lane + 64 * q] = *stg(lane + 64 * q);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1326,10 +1331,12 @@ struct TableEntry {
 std::mutex g_tab_mu;
 std::vector<TableEntry> g_tabs;
 
-// Device copy of the tables for (device, geometry); allocated once per geometry and device.
-int device_tables(const Geometry& g, int expect_words, const uint32_t** out) {
+// Device copy of the tables for (device, geometry); allocated once per geometry and device.  The
+// device is the launch stream's (not the calling thread's current device), so a kernel never reads
+// tables that live on another GPU.
+int device_tables(const Geometry& g, int expect_words, hipStream_t stream, const uint32_t** out) {
   int dev = 0;
-  hipError_t he = hipGetDevice(&dev);
+  hipError_t he = stream ? hipStreamGetDevice(stream, &dev) : hipGetDevice(&dev);
   if (he != hipSuccess) return hip_err(he);
   std::lock_guard<std::mutex> lk(g_tab_mu);
   for (auto& t : g_tabs)
@@ -1340,10 +1347,14 @@ int device_tables(const Geometry& g, int expect_words, const uint32_t** out) {
   int bad = 0;
   std::vector<uint32_t> w = build_tables(g, &bad);
   if (bad || (int)w.size() != expect_words) return WH_ENOTSUP;
+  int cur = 0;
+  he = hipGetDevice(&cur);
+  if (he != hipSuccess) return hip_err(he);
+  if (cur != dev && (he = hipSetDevice(dev)) != hipSuccess) return hip_err(he);
   uint32_t* d = nullptr;
   he = hipMalloc(&d, w.size() * 4);
-  if (he != hipSuccess) return hip_err(he);
-  he = hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  if (cur != dev) hipSetDevice(cur);
   if (he != hipSuccess) return hip_err(he);
   TableEntry t{dev, g.D, g.NR, (int)w.size(), {0}, d};
   memcpy(t.racks, g.racks, sizeof(int) * g.NR);
@@ -1381,6 +1392,9 @@ Kernels make_kernels() {
 }
 
 const std::vector<Kernels>& registry() {
+#ifdef WH_ONLY_MEDIUM8   // analysis builds (tools/lds_stalls.py): one instance, fast to compile
+  static const std::vector<Kernels> r = {make_kernels<16, 9, 3, 8>()};
+#else
   static const std::vector<Kernels> r = {
       // WarehouseSmall  (variants.py:19-32): D=12, R=4, racks [4, 8]
       make_kernels<12, 4, 2, 2>(), make_kernels<12, 4, 2, 4>(),
@@ -1391,6 +1405,7 @@ const std::vector<Kernels>& registry() {
       make_kernels<20, 16, 4, 2>(), make_kernels<20, 16, 4, 4>(), make_kernels<20, 16, 4, 8>(),
       make_kernels<20, 16, 4, 16>(),
   };
+#endif
   return r;
 }
 
@@ -1402,13 +1417,14 @@ const Kernels* pick(const Geometry& g) {
   return best;
 }
 
-int prepare(const wh_config* cfg, int64_t B, Geometry* g, const Kernels** kk, const uint32_t** tab) {
+int prepare(const wh_config* cfg, int64_t B, void* stream, Geometry* g, const Kernels** kk,
+            const uint32_t** tab) {
   int rc = validate(cfg, g);
   if (rc) return rc;
   if (B < 0) return WH_EINVAL;
   *kk = pick(*g);
   if (!*kk) return WH_ENOTSUP;
-  return device_tables(*g, (*kk)->tblw, tab);
+  return device_tables(*g, (*kk)->tblw, (hipStream_t)stream, tab);
 }
 
 inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + BT - 1) / BT)); }
@@ -1477,7 +1493,7 @@ int wh_reset(const wh_config* cfg, int64_t B, uint32_t* state, const uint8_t* ma
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
-  int rc = prepare(cfg, B, &g, &k, &tab);
+  int rc = prepare(cfg, B, stream, &g, &k, &tab);
   if (rc) return rc;
   if (B == 0) return WH_OK;
   if (!state) return WH_EINVAL;
@@ -1496,7 +1512,7 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
-  int rc = prepare(cfg, B, &g, &k, &tab);
+  int rc = prepare(cfg, B, stream, &g, &k, &tab);
   if (rc) return rc;
   if (policy < 0 || policy > 2) return WH_EINVAL;
   if (B == 0) return WH_OK;
@@ -1507,8 +1523,10 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   a.T = g.T;
   a.W = g.W;
   a.tables = tab;
+#ifdef WH_ABLATION
   const char* abl = getenv("WH_ABLATE");   // timing experiments only (tools/ablate.py)
   a.ablate = abl ? atoi(abl) : 0;
+#endif
   void (*kern)(StepParams) = (a.order != nullptr && policy == POL_EXTERNAL) ? k->step_ordered : k->step[policy];
   hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());
@@ -1578,7 +1596,7 @@ int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* ob
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
-  int rc = prepare(cfg, B, &g, &k, &tab);
+  int rc = prepare(cfg, B, stream, &g, &k, &tab);
   if (rc) return rc;
   if (B == 0) return WH_OK;
   if (!state || !obs) return WH_EINVAL;

@@ -240,6 +240,27 @@ class BatchedWarehouse:
                    None if self.stats is None else self.stats.ref, int(bool(autoreset)),
                    int(self.train), self.seed, self.env_offset, self.stream)
 
+    def rollout_launcher(self, steps: int, policy: str = "greedy", p: float = 0.0, rewards=None,
+                         dones=None, returns=None, autoreset: bool = True):
+        """rollout() with every argument bound once: returns a zero-argument callable that launches
+        the same fused rollout with no per-call argument handling (the tensors must stay alive and
+        in place while the callable is used)."""
+        for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
+                         (returns, (self.B,))):
+            if t is not None and tuple(t.shape) != shape:
+                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+        fn = nat.lib().wh_rollout
+        args = (self._cfgp, self.B, self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
+                nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
+                None if self.stats is None else self.stats.ref, int(bool(autoreset)), int(self.train),
+                self.seed, self.env_offset, self.stream)
+
+        def launch() -> None:
+            rc = fn(*args)
+            if rc:
+                nat.check(rc, "wh_rollout")
+        return launch
+
     # ------------------------------------------------------------------ canonical state
     def to_canonical(self) -> Dict[str, torch.Tensor]:
         B, NA, P = self.B, self.agent_slots, self.P

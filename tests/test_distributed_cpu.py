@@ -1,6 +1,8 @@
-"""The multi-GPU path on CPU with gloo, world size 2: bench.py's sharding (rank r owns global env
-ids [r*B, (r+1)*B)), its barrier + max-over-ranks timing window, and the shard-invariance contract
-(philox draws keyed by global env id) checked with the oracle standing in for each rank's GPU."""
+"""The multi-GPU path on CPU with gloo, world size 2, through bench.py's own plumbing: rank_info()
+from the torch.distributed.run environment, shard_offset() (rank r owns global env ids
+[r*B, (r+1)*B)), timed_window() (barrier + sync on both sides, max over ranks) and aggregate_rate();
+the shard-invariance contract (philox draws keyed by global env id) is checked with the oracle
+standing in for each rank's GPU."""
 import os
 import socket
 
@@ -22,32 +24,45 @@ def _free_port():
 
 
 def _worker(rank, world, port, B, steps, out):
+    import time
+
     import torch
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    w, r, local = bench.rank_info()
+    assert (w, r, local) == (world, rank, rank)
+    dist.init_process_group("gloo", rank=r, world_size=w)
     L = oc.layout_for("medium")
-    ids = np.arange(rank * B, (rank + 1) * B)          # bench.py: env_offset = rank * B
+    off = bench.shard_offset(r, B)
+    ids = np.arange(off, off + B)
     S = ob.BState.zeros(L, B, 8)
     d = ob.PhiloxDraws(1234, ids)
     ob.reset(L, S, d)
-    dist.barrier()
-    total = 0.0
-    for _ in range(steps):
-        rew, done, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
-        total += float(rew.sum())
-        if done.any():
-            ob.reset(L, S, d, mask=done)
-    elapsed = torch.tensor([float(rank + 1)], dtype=torch.float64)   # stand-in per-rank time
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    acc = {"total": 0.0}
+
+    def run():
+        for _ in range(steps):
+            rew, done, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+            acc["total"] += float(rew.sum())
+            if done.any():
+                ob.reset(L, S, d, mask=done)
+        time.sleep(0.2 * (r + 1))        # rank 1 is the slow one: the window is its time
+
+    syncs = []
+    elapsed = bench.timed_window(run, lambda: syncs.append(1), w, dist)
+    assert len(syncs) == 2                         # device sync on both sides of the window
+    rate = bench.aggregate_rate(w, B, 8, steps, elapsed)
     pos = torch.from_numpy(S.pos.copy())
-    gathered = [torch.zeros_like(pos) for _ in range(world)]
+    gathered = [torch.zeros_like(pos) for _ in range(w)]
     dist.all_gather(gathered, pos)
-    tot = torch.tensor([total], dtype=torch.float64)
+    tot = torch.tensor([acc["total"]], dtype=torch.float64)
     dist.all_reduce(tot)
-    if rank == 0:
+    if r == 0:
         np.save(out, np.concatenate([g.numpy() for g in gathered]))
-        np.save(out + ".meta.npy", np.array([elapsed.item(), tot.item()]))
+        np.save(out + ".meta.npy", np.array([elapsed, tot.item(), rate]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,8 +73,9 @@ def test_two_rank_shards_equal_single_batch(tmp_path):
     out = str(tmp_path / "pos.npy")
     mp.start_processes(_worker, args=(world, _free_port(), B, steps, out), nprocs=world, start_method="spawn")
     sharded = np.load(out)
-    elapsed, total = np.load(out + ".meta.npy")
-    assert elapsed == 2.0                              # max over ranks
+    elapsed, total, rate = np.load(out + ".meta.npy")
+    assert elapsed >= 0.4                              # max over ranks: rank 1 slept 0.4 s
+    assert rate == pytest.approx(world * B * 8 * steps / elapsed)
     L = oc.layout_for("medium")
     S = ob.BState.zeros(L, world * B, 8)
     d = ob.PhiloxDraws(1234, np.arange(world * B))

@@ -1,0 +1,7 @@
+#!/bin/bash
+# round-2 first GPU call: op-rate probe, launch-cost breakdown, GPU tests, driver bench, rocprof
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+bash tools/gpu_round.sh "tools/oprate4_bin" "python tools/launch_cost.py" \
+  "python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread" \
+  "python bench.py --gpus 1 --steps 20 --warmup 5" \
+  "bash tools/prof_driver.sh r02_driver"
