@@ -193,11 +193,12 @@ def aggregate_rate(world, envs_per_gpu, agents, steps, elapsed):
     return world * envs_per_gpu * agents * steps / elapsed
 
 
-def window_setup_steps(T, K, W):
-    """Untimed steps before the warmup so that the timed window [s+W, s+W+K) is centred on an
-    episode end (t = T: done, auto-reset, and the expiry of the reset-time requests, core.py:303-306,
-    438): s + W + K//2 = T (mod T)."""
-    return (T - (K // 2) % T - W) % T
+def window_setup_steps(T, K, pre):
+    """Untimed positioning steps so that the timed window, which starts after `pre` other steps
+    (capture warm-up, the dry run, the warmup), is centred on an episode end (t = T: done,
+    auto-reset, and the expiry of the reset-time requests, core.py:303-306, 438):
+    setup + pre + K//2 = T (mod T)."""
+    return (T - (K // 2) % T - pre) % T
 
 
 def launch_plan(K, chunk):
@@ -211,31 +212,33 @@ def launch_plan(K, chunk):
 def measure(env, mode, policy, K, W, chunk, dev, world, dist):
     """Time K steps of `mode` (the contract's window).  The kernel time comes from HIP events recorded
     on the launch stream INSIDE that window around exactly the timed launches, so the roofline
-    describes the launches that were timed.  Returns a dict."""
+    describes the launches that were timed.  Before the warmup, one untimed dry run of the same
+    launches, events and synchronisation warms the host path (it is part of the setup steps).
+    Returns a dict."""
     import torch
 
     B, NA = env.B, env.agent_slots
     T = int(env.geometry["T"])
     stream = torch.cuda.current_stream(dev)
-    setup = window_setup_steps(T, K, W)
-    if setup:
-        env.rollout(setup, policy, 0.0)           # position the window (untimed, no outputs)
     whole = K * B * (NA * 4 + 1) <= (4 << 30)     # per-step outputs of the whole window fit: keep them all
+    pre = 0
     if mode == "graph":
         rew1 = torch.zeros((1, B, NA), device=dev)
         dn1 = torch.zeros((1, B), dtype=torch.uint8, device=dev)
+
         def one():   # reads the current stream per call: the capture runs on a side stream
             env.rollout(1, policy, 0.0, rewards=rew1, dones=dn1)
 
-        for _ in range(max(W, 3)):
+        for _ in range(3):
             one()
+        pre += 3
         torch.cuda.synchronize(dev)
         G = min(K, 200)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for _ in range(G):
                 one()
-        # capture replays nothing: the G captured steps run only in the timed window
+        # capture replays nothing: the G captured steps run only when replayed
         torch.cuda.synchronize(dev)
         tail = env.rollout_launcher(1, policy, 0.0, rewards=rew1, dones=dn1)
         launches = [graph.replay] * (K // G) + [tail] * (K % G)
@@ -254,12 +257,6 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist):
             o = off if whole else 0
             launches.append(env.rollout_launcher(c, policy, 0.0, rewards=rew[o:o + c], dones=dn[o:o + c]))
             off += c
-        if W:
-            wr = torch.zeros((min(W, chunk), B, NA), device=dev)
-            wd = torch.zeros((min(W, chunk), B), dtype=torch.uint8, device=dev)
-            for c in launch_plan(W, chunk):
-                env.rollout(c, policy, 0.0, rewards=wr[:c], dones=wd[:c])
-            del wr, wd
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run():
@@ -268,16 +265,28 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist):
             launch()
         ev1.record(stream)
 
+    timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)     # dry run (setup)
+    pre += K
+    setup = window_setup_steps(T, K, pre + W)
+    if setup:
+        env.rollout(setup, policy, 0.0)           # position the window (untimed, no outputs)
+    if W:
+        wr = torch.zeros((min(W, chunk), B, NA), device=dev)
+        wd = torch.zeros((min(W, chunk), B), dtype=torch.uint8, device=dev)
+        for c in launch_plan(W, chunk):
+            env.rollout(c, policy, 0.0, rewards=wr[:c], dones=wd[:c])
+        del wr, wd
     elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
     span_ms = ev0.elapsed_time(ev1)
     kernels = len(plan)
     bytes_total = sum(B * (2 * 4 * env.layout.words_per_env + c * (4 * NA + 1)) for c in plan)
     dones = int(dn.sum().item()) if (dn is not None and whole) else None
+    start = (pre + setup + W) % T
     return dict(elapsed=elapsed, span_ms=span_ms, kernel_ms=span_ms / kernels, launches=kernels,
                 steps_per_launch=plan[0], bytes_per_launch=bytes_total / kernels,
                 achieved_gbs=bytes_total / (span_ms * 1e-3) / 1e9, bytes_per_env_step=bytes_total / (B * K),
-                host_fixed_us=(elapsed * 1e3 - span_ms) * 1e3, setup_steps=setup,
-                window_t=[(setup + W) % T, (setup + W + K) % T], dones_in_window=dones)
+                host_fixed_us=(elapsed * 1e3 - span_ms) * 1e3, setup_steps=pre + setup,
+                window_t=[start, (start + K) % T], dones_in_window=dones)
 
 
 def measure_sampler(env, K, W, dev, world, dist):
@@ -504,8 +513,9 @@ def main():
                 "parallelism": f"independent env shards x{world}, no collectives",
                 "window": {"setup_steps": m["setup_steps"], "t_at_start_end": m["window_t"],
                            "dones_in_window": m["dones_in_window"],
-                           "note": "untimed setup steps place the timed window across an episode end "
-                                   "(done + auto-reset + request expiry inside it)"},
+                           "note": "untimed setup steps (including one dry run of the timed launches) place "
+                                   "the timed window across an episode end (done + auto-reset + request "
+                                   "expiry inside it)"},
             },
             "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,

@@ -276,31 +276,46 @@ __device__ __forceinline__ uint64_t low_mask() {
   return N >= 64 ? ~0ull : ((1ull << N) - 1ull);
 }
 
+// The packed words of one env, loaded to registers.  Issued before the workgroup's table load so
+// the two memory latencies of the prologue overlap (vmcnt retires in order: the table wait covers
+// these loads too).
 template <class C>
-__device__ __forceinline__ void load_env(Regs<C>& s, Lds<C>& L, const uint32_t* __restrict__ st, int64_t B,
-                                         int64_t e, int na, uint32_t W, int tid) {
-  s.hdr = st[e];
-  s.epi = st[B + e];
+struct RawEnv {
+  uint32_t hdr, epi, ag[C::NAM], pt[C::PW], pm[C::PW];
+};
+
+template <class C>
+__device__ __forceinline__ void load_env_issue(RawEnv<C>& r, const uint32_t* __restrict__ st, int64_t B,
+                                               int64_t e, int na) {
+  r.hdr = st[e];
+  r.epi = st[B + e];
 #pragma unroll
-  for (int i = 0; i < C::NAM; ++i) s.ag[i] = (i < na) ? st[(2 + i) * B + e] : IDLE;
+  for (int i = 0; i < C::NAM; ++i) r.ag[i] = (i < na) ? st[(2 + i) * B + e] : IDLE;
   const int wpt = 2 + na;
-  uint32_t pt[C::PW], pm[C::PW];
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) pt[w] = st[(wpt + w) * B + e];
+  for (int w = 0; w < C::PW; ++w) r.pt[w] = st[(wpt + w) * B + e];
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) pm[w] = st[(wpt + C::PW + w) * B + e];
+  for (int w = 0; w < C::PW; ++w) r.pm[w] = st[(wpt + C::PW + w) * B + e];
+}
+
+template <class C>
+__device__ __forceinline__ void load_env_finish(Regs<C>& s, Lds<C>& L, const RawEnv<C>& r, uint32_t W, int tid) {
+  s.hdr = r.hdr;
+  s.epi = r.epi;
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i) s.ag[i] = r.ag[i];
 #pragma unroll
   for (int j = 0; j < C::P; ++j)
-    L.pkp[j][tid] = (uint16_t)(((pt[j >> 2] >> (8 * (j & 3))) & 0xFFu) | (((pm[j >> 2] >> (8 * (j & 3))) & 0xFFu) << 8));
-  s.am = active_mask<C>(pt);
+    L.pkp[j][tid] = (uint16_t)(((r.pt[j >> 2] >> (8 * (j & 3))) & 0xFFu) | (((r.pm[j >> 2] >> (8 * (j & 3))) & 0xFFu) << 8));
+  s.am = active_mask<C>(r.pt);
   // expiry step of each open request: t + (expiry byte - t) mod 256, as the expiry phase counts
   const uint32_t t0 = s.hdr & 0xFFFFu;
   bool early = false;
 #pragma unroll
   for (int j = 0; j < C::P; ++j) {
     const uint32_t sh = 8 * (j & 3);
-    const uint32_t rem = (((pm[j >> 2] >> sh) & 0xFFu) - t0) & 0xFFu;
-    early |= ((pt[j >> 2] >> sh) & 0xFFu) != 0u && t0 + rem < W;
+    const uint32_t rem = (((r.pm[j >> 2] >> sh) & 0xFFu) - t0) & 0xFFu;
+    early |= ((r.pt[j >> 2] >> sh) & 0xFFu) != 0u && t0 + rem < W;
   }
   s.wskip = __any(early) ? 0u : W;
 }
@@ -479,7 +494,9 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
 // core.py:267-368 on one env held in registers.  Returns done.  No data-dependent branches:
 // LDS side effects are predicated through neutral operands (and ~0 / or 0 / the scratch word),
 // so each phase is one basic block and its LDS reads issue back to back.
-template <class C, bool ORDERED>
+// INJ = false compiles the injected-draw regeneration out (the fused rollout and the sampler step
+// always draw from philox): less code in the step loop and no per-step test of `regen`.
+template <class C, bool ORDERED, bool INJ = true>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
                                          const int32_t* __restrict__ actions_g,
@@ -680,10 +697,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       uint4 blk = make_uint4(0u, 0u, 0u, 0u);   // words 2j (pickup) and 2j+1 (target) share a block
 #pragma unroll
       for (int j = 0; j < C::R; ++j) {
-        if (__any(j < kreq)) {                  // wave-uniform: skip items no env needs
+        // wave-uniform: once no env needs item j, none needs a later one -- leave the loop (one
+        // branch test per executed item + 1, instead of one per item)
+        if (!__any(j < kreq)) break;
+        {
           uint32_t ma = sgn((uint32_t)j - (uint32_t)kreq);   // j < kreq
           uint32_t sel, tgi;
-          if (regen) {
+          if (INJ && regen) {
             const uint32_t rpos = (uint32_t)regen[e * 2 * C::R + j];
             tgi = (uint32_t)regen[e * 2 * C::R + C::R + j];
             const bool valid = rpos < nin && tgi < (uint32_t)C::DP;   // invalid draws are ignored
@@ -913,19 +933,64 @@ __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C
   if (stats) a.stats.episode_return[e] = epr;
 }
 
-template <class C, int POLICY, bool ORDERED>
+// The fused rollout's common case as its own instance: wh_rollout with rewards + dones written,
+// auto-reset on, no returns / episode stats / env mask, na == NAM with NAM even (16/8-byte reward
+// rows).  No per-step tests of launch options, and the injected-draw path is compiled out, so a
+// step executes few branch instructions -- each costs several issue slots at one wave per SIMD
+// (tools/oprate5.hip: ~8 ns per s_cbranch/s_branch against ~2.6 ns per VALU op).
+template <class C>
+__device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]) {
+  if constexpr ((C::NAM & 3) == 0) {
+#pragma unroll
+    for (int q = 0; q < C::NAM / 4; ++q)
+      reinterpret_cast<float4*>(row)[q] = make_float4(rew[4 * q], rew[4 * q + 1], rew[4 * q + 2], rew[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < C::NAM / 2; ++q) reinterpret_cast<float2*>(row)[q] = make_float2(rew[2 * q], rew[2 * q + 1]);
+  }
+}
+
+template <class C, int POLICY>
+__device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, Lds<C>& L, const Keys& k,
+                                               uint32_t gid, int64_t e, int tid) {
+  float* rrow = a.rewards + e * C::NAM;
+  uint8_t* drow = a.dones + e;
+  const int64_t rstride = a.B * C::NAM;
+  for (int stp = 0; stp < a.steps; ++stp) {
+    uint32_t d[C::NAM];
+    policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+    float rew[C::NAM];
+    const bool done = step_env<C, false, false>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, 0);
+    store_row<C>(rrow, rew);
+    *drow = done ? 1 : 0;
+    rrow += rstride;
+    drow += a.B;
+    if (__any(done)) {           // wave-uniform test first: one branch on the common path
+      if (done) {
+        reset_philox<C>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+#pragma unroll
+        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+      }
+    }
+  }
+}
+
+template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
-  load_tables<C>(L.tbl, a.tables);
-  __syncthreads();
   const int tid = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
-  if (e >= a.B) return;
-  if (a.mask && !a.mask[e]) return;
+  const bool live = e < a.B && (FAST || !a.mask || a.mask[e]);
+  RawEnv<C> raw;
+  if (live) load_env_issue<C>(raw, a.state, a.B, e, a.na);
+  load_tables<C>(L.tbl, a.tables);
+  __syncthreads();
+  if (!live) return;
   const Keys k{a.k0, a.k1};
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
-  load_env<C>(s, L, a.state, a.B, e, a.na, (uint32_t)a.W, tid);
+  load_env_finish<C>(s, L, raw, (uint32_t)a.W, tid);
   // Drain the state loads here.  Their first uses are inside the step loop, so otherwise the
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
@@ -933,7 +998,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
 #pragma unroll
   for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
 
-  if (a.phase == PH_POLICY) {
+  if (!FAST && a.phase == PH_POLICY) {
     uint32_t d[C::NAM];
     policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
     const uint32_t n = (s.hdr >> 16) & 0xFFu;
@@ -943,7 +1008,9 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     return;
   }
 
-  if (!ORDERED && a.phase == PH_ALL)
+  if (FAST)
+    run_steps_fast<C, POLICY>(a, s, L, k, gid, e, tid);
+  else if (!ORDERED && a.phase == PH_ALL)
     run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
@@ -1354,7 +1421,7 @@ int device_tables(const Geometry& g, int expect_words, hipStream_t stream, const
   uint32_t* d = nullptr;
   he = hipMalloc(&d, w.size() * 4);
   if (he == hipSuccess) he = hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice);
-  if (cur != dev) hipSetDevice(cur);
+  if (cur != dev) (void)hipSetDevice(cur);
   if (he != hipSuccess) return hip_err(he);
   TableEntry t{dev, g.D, g.NR, (int)w.size(), {0}, d};
   memcpy(t.racks, g.racks, sizeof(int) * g.NR);
@@ -1367,6 +1434,7 @@ int device_tables(const Geometry& g, int expect_words, hipStream_t stream, const
 struct Kernels {
   int D, R, NR, NAM;
   void (*step[3])(StepParams);
+  void (*step_fast[3])(StepParams);   // [policy]: greedy / random fused rollouts (NAM even), else null
   void (*step_ordered)(StepParams);
   void (*reset)(ResetParams);
   void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int);   // 8 / 16 / 64 envs per WG
@@ -1378,10 +1446,17 @@ Kernels make_kernels() {
   using C = Cfg<D, R, NR, NAM>;
   Kernels k;
   k.D = D; k.R = R; k.NR = NR; k.NAM = NAM;
-  k.step[0] = k_step<C, POL_EXTERNAL, false>;
-  k.step[1] = k_step<C, POL_GREEDY, false>;
-  k.step[2] = k_step<C, POL_RANDOM, false>;
-  k.step_ordered = k_step<C, POL_EXTERNAL, true>;
+  k.step[0] = k_step<C, POL_EXTERNAL, false, false>;
+  k.step[1] = k_step<C, POL_GREEDY, false, false>;
+  k.step[2] = k_step<C, POL_RANDOM, false, false>;
+  k.step_fast[0] = nullptr;
+  if constexpr (NAM % 2 == 0) {
+    k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
+    k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
+  } else {
+    k.step_fast[1] = k.step_fast[2] = nullptr;
+  }
+  k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
   k.observe[0] = k_observe<C, 8>;
   k.observe[1] = k_observe<C, 16>;
@@ -1528,6 +1603,12 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   a.ablate = abl ? atoi(abl) : 0;
 #endif
   void (*kern)(StepParams) = (a.order != nullptr && policy == POL_EXTERNAL) ? k->step_ordered : k->step[policy];
+  // the fused rollout's common case (run_steps_fast); rows of 16 (NAM % 4 == 0) or 8 bytes
+  const uintptr_t ralign = (k->NAM % 4 == 0) ? 15u : 7u;
+  if (k->step_fast[policy] && a.phase == PH_ALL && a.rewards && a.dones && !a.returns &&
+      !a.stats.episode_return && !a.mask && !a.order && !a.regen && !a.n_inactive && a.autoreset &&
+      g.NA == k->NAM && ((uintptr_t)a.rewards & ralign) == 0 && a.ablate == 0)
+    kern = k->step_fast[policy];
   hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());
 }

@@ -34,7 +34,8 @@ def main():
     ap.add_argument("prof_dir")
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="k_step")
-    ap.add_argument("--round", default="r01")
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--steps-per-launch", type=int, default=None)
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -44,7 +45,12 @@ def main():
     for r in csv.DictReader(open(stats)):
         if r["Name"].startswith(a.kernel):
             avg_ns = float(r["AverageNs"])
-    out = {"kernel": a.kernel, "avg_ns": avg_ns, "round": a.round}
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+
+    out = {"kernel": a.kernel, "avg_ns": avg_ns, "round": a.round, "source_sha": bench.source_sha(),
+           "steps_per_launch": a.steps_per_launch}
     fetch, n_f = counters(os.path.join(a.prof_dir, "fetch", "run_counter_collection.csv"), a.kernel)
     write, n_w = counters(os.path.join(a.prof_dir, "write", "run_counter_collection.csv"), a.kernel)
     out["fetch_kb"] = fetch.get("FETCH_SIZE")
@@ -52,10 +58,11 @@ def main():
     out["dispatches"] = {"fetch": n_f.get("FETCH_SIZE"), "write": n_w.get("WRITE_SIZE")}
     if out["fetch_kb"] is not None and out["write_kb"] is not None:
         out["bytes_per_launch"] = (2 * out["fetch_kb"] + out["write_kb"]) * 1024
-    extra = os.path.join(a.prof_dir, "sq", "run_counter_collection.csv")
-    if os.path.exists(extra):
-        sq, _ = counters(extra, a.kernel)
-        out["sq"] = sq
+    for sub in ("sq", "sq2"):
+        extra = os.path.join(a.prof_dir, sub, "run_counter_collection.csv")
+        if os.path.exists(extra):
+            sq, _ = counters(extra, a.kernel)
+            out.setdefault("sq", {}).update(sq)
     path = os.path.join(prof, "pmc_traffic.json")
     d = json.load(open(path)) if os.path.exists(path) else {}
     d[a.tag] = out
