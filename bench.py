@@ -16,7 +16,8 @@ Rank 0 prints ONE JSON line.  Besides the contract fields it carries
                   (it writes B*NA*(9R+1)*4 bytes per step: HBM-write bound)
   policy_path  -- scripts/rollout.py's loop with the SAC policy network on the device
                   (wh_mlp_forward over all agent rows, then wh_vector_step), with the MLP kernel's
-                  MFMA roofline (dense bf16 peak)
+                  MFMA roofline (dense bf16 peak); policy_path_f32 the same with the exact-f32
+                  network (f32 MFMA peak)
   roofline     -- algorithmic bytes of the step kernel / its mean duration (HIP events on the
                   launch stream), against the 8 TB/s HBM peak; `traffic` from the committed
                   rocprofv3 PMC summary (profiles/) when present.
@@ -39,6 +40,7 @@ for _p in (ROOT, os.path.join(ROOT, "rllib-warehouse_amd")):
 METRIC = "agent-steps/sec (aggregate) at B=65536 envs × 8 agents, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
 MFMA_BF16_PEAK_TFS = 2500.0   # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+MFMA_F32_PEAK_TFS = 157.3     # f32-input MFMA peak (= the f32 vector rate), MI355X_MICROARCH.md
 
 
 def cpu_worker(args):
@@ -329,7 +331,7 @@ def measure_sampler(env, K, W, dev, world, dist):
     return elapsed, kms[len(kms) // 2]
 
 
-def measure_policy(env, K, W, dev, world, dist):
+def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     """scripts/rollout.py's loop on the device: per step the SAC policy network
     (wh_mlp_forward, argmax) over all B x NA observation rows, then wh_vector_step (step +
     auto-reset + next rows).  hipGraph of G steps.  Returns (elapsed_s, mlp_kernel_ms, net)."""
@@ -337,7 +339,7 @@ def measure_policy(env, K, W, dev, world, dist):
 
     import warehouse.policy as wp
 
-    net = wp.MLPPolicy(env.variant, seed=7, device=dev)
+    net = wp.MLPPolicy(env.variant, seed=7, device=dev, precision=precision)
     B, NA = env.B, env.agent_slots
     acts = torch.empty((B, NA), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -421,6 +423,7 @@ def main():
     ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
     ap.add_argument("--no-policy", action="store_true", help="skip the SAC-policy rollout measurement")
     ap.add_argument("--policy-steps", type=int, default=200)
+    ap.add_argument("--policy-steps-f32", type=int, default=40)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = one per host core (host_cores())")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -472,23 +475,30 @@ def main():
                          "traffic": load_traffic(f"{args.variant}_n{NA}_observe")},
         }
 
-    policy_line = None
+    policy_line = policy_f32 = None
     if not args.no_policy:
-        Kp = min(K, args.policy_steps)
-        el4, mms, net = measure_policy(env, Kp, W, dev, world, dist)
         rows = B * NA
-        flop = 2.0 * rows * (net.in_dim * net.hidden[0] + net.hidden[0] * net.hidden[1] + net.hidden[1] * 9)
-        policy_line = {
-            "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
-                        f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset + "
-                        f"observation rows); random-init weights (no checkpoint ships with the reference)",
-            "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,
-            "ms_per_step": el4 * 1e3 / Kp, "dtype": f"{getattr(net, 'precision', 'bf16')} MFMA, f32 accumulate",
-            "roofline": {"bound": "mfma", "kernel": "k_mlp", "kernel_ms": mms, "flop_per_launch": flop,
-                         "achieved": flop / (mms * 1e-3) / 1e12, "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": flop / (mms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS,
-                         "traffic": load_traffic(f"{args.variant}_n{NA}_mlp")},
-        }
+        for prec in ("bf16", "f32"):
+            Kp = min(K, args.policy_steps if prec == "bf16" else args.policy_steps_f32)
+            el4, mms, net = measure_policy(env, Kp, W, dev, world, dist, prec)
+            flop = 2.0 * rows * (net.in_dim * net.hidden[0] + net.hidden[0] * net.hidden[1] + net.hidden[1] * 9)
+            peak = MFMA_BF16_PEAK_TFS if prec == "bf16" else MFMA_F32_PEAK_TFS
+            line = {
+                "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
+                            f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset + "
+                            f"observation rows); random-init weights (no checkpoint ships with the reference)",
+                "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,
+                "ms_per_step": el4 * 1e3 / Kp,
+                "dtype": "bf16 MFMA, f32 accumulate" if prec == "bf16" else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                "roofline": {"bound": "mfma", "kernel": "k_mlp" if prec == "bf16" else "k_mlp_f32", "kernel_ms": mms,
+                             "flop_per_launch": flop, "achieved": flop / (mms * 1e-3) / 1e12, "peak": peak,
+                             "unit": "TFLOP/s", "frac": flop / (mms * 1e-3) / 1e12 / peak,
+                             "traffic": load_traffic(f"{args.variant}_n{NA}_mlp" + ("" if prec == "bf16" else "_f32"))},
+            }
+            if prec == "bf16":
+                policy_line = line
+            else:
+                policy_f32 = line
 
     if rank == 0:
         out = {
@@ -521,6 +531,7 @@ def main():
             "alt_launch_mode": alt,
             "sampler_path": sampler,
             "policy_path": policy_line,
+            "policy_path_f32": policy_f32,
         }
         if not args.no_cpu_baseline and world == 1:   # reported at N=1 only
             cores, detail = host_cores()

@@ -172,11 +172,17 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
 
 /* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a
  * ReLU MLP, hidden_layer_sizes [256,256] Small / [512,512] Medium / [1024,256] Large, 9 action
- * logits), i.e. trainer.compute_action(obs) of scripts/rollout.py:84-86 for every agent row of a
- * batch.  bf16 MFMA with f32 accumulation; activations are rounded to bf16 between layers.
- * Supported: in_dim = 9R+1 of a variant with its hidden sizes, out_dim = 9 (else WH_ENOTSUP). */
+ * logits), i.e. trainer.compute_action(obs) of scripts/rollout.py:72 for every agent row of a
+ * batch.  precision WH_MLP_BF16: bf16 MFMA with f32 accumulation, activations rounded to bf16
+ * between layers (fast); WH_MLP_F32: exact f32 (v_mfma_f32_32x32x2_f32, an fmaf chain per output:
+ * logits equal a float32 reference up to summation order), like the reference's TF fp32 policy.
+ * Supported: in_dim = 9R+1 of a variant with its hidden sizes, out_dim = 9 (else WH_ENOTSUP).
+ * Blobs are precision-specific: pack and forward with the same desc. */
+#define WH_MLP_BF16 0
+#define WH_MLP_F32 1
 typedef struct wh_mlp_desc {
   int32_t in_dim, hidden0, hidden1, out_dim;
+  int32_t precision; /* WH_MLP_BF16 or WH_MLP_F32 */
 } wh_mlp_desc;
 
 /* Size of the packed weight blob (device bytes).  Host only. */
@@ -197,6 +203,13 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
 
 /* Library build identification (e.g. "warehouse_amd gfx950 <date>"). */
 const char* wh_version(void);
+
+/* Assert-mode builds (-DWH_CHECK) check SURVEY §5's invariants inside the kernels after every
+ * state load, step and reset: exactly R open requests, live agents inside the grid, carried
+ * targets on delivery cells, request bytes valid delivery indices, open mask == table, n <= slots.
+ * out[4] = {violations, first failing env id, its failed-check bits, env-states checked}; clear
+ * != 0 zeroes the counters.  Synchronises the current device.  WH_ENOTSUP in production builds. */
+int wh_check_read(uint64_t* out, int32_t clear);
 
 #ifdef __cplusplus
 }

@@ -189,6 +189,58 @@ __device__ __forceinline__ void layer1(const u32x4* S, const bf16x8 (&hb)[N::CH]
   }
 }
 
+// Logit o of sample r sits in the output tile as: o 0-3 in lane r regs 0-3, o 4-7 in lane r+32
+// regs 0-3, o 8 in lane r reg 4 (C/D map row = (reg&3) + 8(reg>>2) + 4(lane>>5)).  Adds b2, then
+// writes logits and/or the argmax (first maximum) or a Gumbel-max sample.
+__device__ __forceinline__ void emit_logits(const f32x16& lg, const float* b2, int64_t row, bool live, int h,
+                                            const MlpArgs& a) {
+  float up[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) up[e] = __shfl_xor(lg[e], 32);
+  if (h == 0 && live) {
+    constexpr int OUT = 9;
+    float z[OUT];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      z[e] = lg[e] + b2[e];
+      z[4 + e] = up[e] + b2[4 + e];
+    }
+    z[8] = lg[4] + b2[8];
+    if (a.logits) {
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) a.logits[row * OUT + o] = z[o];
+    }
+    if (a.actions) {
+      float best = -INFINITY;
+      int arg = 0;
+      if (a.explore) {
+        // Gumbel-max: argmax(z + g), g = -log(-log u), u in (0,1) from philox(row, step)
+        uint32_t u32[12];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
+                                   a.k0, a.k1);
+          u32[4 * b] = v.x;
+          u32[4 * b + 1] = v.y;
+          u32[4 * b + 2] = v.z;
+          u32[4 * b + 3] = v.w;
+        }
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+          const float v = z[o] - __logf(-__logf(u));
+          if (v > best) { best = v; arg = o; }
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < OUT; ++o)
+          if (z[o] > best) { best = z[o]; arg = o; }   // first maximum wins (numpy/torch argmax)
+      }
+      a.actions[row] = arg;
+    }
+  }
+}
+
 template <class N>
 __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
   // two weight stages + both hidden biases; A fragments are ds_read_b128 at operand*1 KiB +
@@ -275,52 +327,109 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
       }
     }
 
-    // logit o of sample r: o 0-3 in lane r regs 0-3, o 4-7 in lane r+32 regs 0-3, o 8 in lane r reg 4
-    float up[4];
+    emit_logits(lg, b2, row, live, h, a);
+  }
+}
+
+// ------------------------------------------------------------------------------------- f32 mode
+// The same network in exact f32 (the reference policy is TF fp32): every layer on
+// v_mfma_f32_32x32x2_f32, whose result is bit-for-bit a k-ordered f32 fmaf chain, so logits differ
+// from a float32 reference only by summation order (~1e-7 relative).  Same orientation as the
+// bf16 kernel: a wave's 32 samples are the tile COLUMNS, so a 32x32 f32 accumulator register g
+// (rows (g&3) + 8(g>>2) + 4h on lane half h) is, after bias + ReLU, directly the B operand of one
+// K = 2 step of the next layer -- the k pair (r_g, r_g + 4) is folded into the packed weights.
+// Weights stream from L2 as one 256-byte A operand per MFMA, in exactly the order the MFMAs
+// consume them, through a 16-deep register ring (a load issued 16 MFMAs = ~1,000 cycles ahead).
+template <int IN_, int H0_, int H1_, int PASSES_>
+struct NetF {
+  static constexpr int IN = IN_, H0 = H0_, H1 = H1_, PASSES = PASSES_, OUT = 9;
+  static constexpr int KS0 = (IN + 1) / 2;                 // layer-0 K = 2 steps
+  static constexpr int KS0P = (KS0 + 15) / 16 * 16;        // padded so every segment is 16 ops long
+  static constexpr int T0 = H0 / 32, T1 = H1 / 32, T1P = T1 / PASSES;
+  static constexpr int RING = 16;
+  // operand stream (64 f32 per op, lane-linear): per pass { per layer-0 tile t: W0 [KS0P],
+  // W1 [16 g][T1P u] }, then W2 [T1P u][16 g]; RING zero ops of read-ahead padding; then f32
+  // biases b0[H0], b1[H1], b2[32]
+  static constexpr int64_t OPS = (int64_t)PASSES * (T0 * (KS0P + 16 * T1P) + 16 * T1P);
+  static constexpr int64_t BIAS_OFF = (OPS + RING) * 256;
+  static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
+  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T1 % PASSES == 0, "tile shapes");
+};
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <class N>
+__global__ __launch_bounds__(256) void k_mlp_f32(MlpArgs a) {
+  __shared__ float bias[N::H0 + N::H1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = lane & 31, h = lane >> 5;
+  const float* ops = static_cast<const float*>(a.packed);
+  const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
+  for (int i = tid; i < N::H0 + N::H1; i += 256) bias[i] = gb[i];
+  __syncthreads();
+  const int64_t task = (int64_t)blockIdx.x * 4 + w;
+  const int64_t row0 = task * 32;
+  if (row0 >= a.rows) return;
+  const int64_t row = row0 + n;
+  const bool live = row < a.rows;
+  // X^T operands: lane (n, h) holds obs[row n][2s + h]
+  float xop[N::KS0P];
+  {
+    const float* x = a.obs + (live ? row : row0) * N::IN;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) up[e] = __shfl_xor(lg[e], 32);
-    if (h == 0 && live) {
-      float z[N::OUT];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        z[e] = lg[e] + b2[e];
-        z[4 + e] = up[e] + b2[4 + e];
-      }
-      z[8] = lg[4] + b2[8];
-      if (a.logits) {
-#pragma unroll
-        for (int o = 0; o < N::OUT; ++o) a.logits[row * N::OUT + o] = z[o];
-      }
-      if (a.actions) {
-        float best = -INFINITY;
-        int arg = 0;
-        if (a.explore) {
-          // Gumbel-max: argmax(z + g), g = -log(-log u), u in (0,1) from philox(row, step)
-          uint32_t u32[12];
-#pragma unroll
-          for (int b = 0; b < 3; ++b) {
-            const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
-                                     a.k0, a.k1);
-            u32[4 * b] = v.x;
-            u32[4 * b + 1] = v.y;
-            u32[4 * b + 2] = v.z;
-            u32[4 * b + 3] = v.w;
-          }
-#pragma unroll
-          for (int o = 0; o < N::OUT; ++o) {
-            const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-            const float v = z[o] - __logf(-__logf(u));
-            if (v > best) { best = v; arg = o; }
-          }
-        } else {
-#pragma unroll
-          for (int o = 0; o < N::OUT; ++o)
-            if (z[o] > best) { best = z[o]; arg = o; }   // first maximum wins (numpy/torch argmax)
-        }
-        a.actions[row] = arg;
-      }
+    for (int q = 0; q < N::KS0P; ++q) {
+      const int k = 2 * q + h;
+      xop[q] = (k < N::IN && live) ? x[k < N::IN ? k : 0] : 0.0f;
     }
   }
+  const float* sp = ops + lane;           // op i of this lane: sp[i * 64]
+  float ring[N::RING];
+#pragma unroll
+  for (int q = 0; q < N::RING; ++q) ring[q] = sp[q * 64];
+  sp += N::RING * 64;                      // sp = the op RING ahead of the next consumed one
+  f32x16 lg{};
+  for (int p = 0; p < N::PASSES; ++p) {
+    f32x16 acc1[N::T1P];
+#pragma unroll
+    for (int u = 0; u < N::T1P; ++u) acc1[u] = f32x16{};
+    for (int t = 0; t < N::T0; ++t) {
+      f32x16 acc0{};
+#pragma unroll
+      for (int q = 0; q < N::KS0P; ++q) {
+        acc0 = mfma_f32(ring[q % N::RING], xop[q], acc0);
+        ring[q % N::RING] = sp[q * 64];
+      }
+      sp += N::KS0P * 64;
+      float hv[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g)
+        hv[g] = fmaxf(acc0[g] + bias[32 * t + (g & 3) + 8 * (g >> 2) + 4 * h], 0.0f);
+#pragma unroll
+      for (int g = 0; g < 16; ++g)
+#pragma unroll
+        for (int u = 0; u < N::T1P; ++u) {
+          const int j = g * N::T1P + u;
+          acc1[u] = mfma_f32(ring[j % N::RING], hv[g], acc1[u]);
+          ring[j % N::RING] = sp[j * 64];
+        }
+      sp += 16 * N::T1P * 64;
+    }
+#pragma unroll
+    for (int u = 0; u < N::T1P; ++u) {
+      const int tile = p * N::T1P + u;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float v = fmaxf(acc1[u][g] + bias[N::H0 + 32 * tile + (g & 3) + 8 * (g >> 2) + 4 * h], 0.0f);
+        const int j = u * 16 + g;
+        lg = mfma_f32(ring[j % N::RING], v, lg);
+        ring[j % N::RING] = sp[j * 64];
+      }
+    }
+    sp += 16 * N::T1P * 64;
+  }
+  emit_logits(lg, gb + N::H0 + N::H1, row, live, h, a);
 }
 
 // ------------------------------------------------------------------------------------- host
@@ -382,8 +491,43 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
   return blob;
 }
 
+template <class N>
+std::vector<uint8_t> pack_f32(const float* w0, const float* b0, const float* w1, const float* b1,
+                              const float* w2, const float* b2) {
+  std::vector<uint8_t> blob(N::BYTES, 0);
+  float* f = reinterpret_cast<float*>(blob.data());
+  int64_t op = 0;
+  auto rg = [](int g) { return (g & 3) + 8 * (g >> 2); };   // accumulator register g -> row (half 0)
+  for (int p = 0; p < N::PASSES; ++p) {
+    for (int t = 0; t < N::T0; ++t) {
+      for (int q = 0; q < N::KS0P; ++q, ++op)        // W0 [H0][IN]: lane (i, h) = W0[32t + i][2q + h]
+        for (int l = 0; l < 64; ++l) {
+          const int i = l & 31, k = 2 * q + (l >> 5);
+          f[op * 64 + l] = k < N::IN ? w0[(int64_t)(32 * t + i) * N::IN + k] : 0.0f;
+        }
+      for (int g = 0; g < 16; ++g)                   // W1 [H1][H0]: k pair (r_g, r_g + 4) of tile t
+        for (int u = 0; u < N::T1P; ++u, ++op)
+          for (int l = 0; l < 64; ++l) {
+            const int i = l & 31, k = 32 * t + rg(g) + 4 * (l >> 5);
+            f[op * 64 + l] = w1[(int64_t)(32 * (p * N::T1P + u) + i) * N::H0 + k];
+          }
+    }
+    for (int u = 0; u < N::T1P; ++u)                 // W2 [9][H1], rows padded to 32 with zeros
+      for (int g = 0; g < 16; ++g, ++op)
+        for (int l = 0; l < 64; ++l) {
+          const int i = l & 31, k = 32 * (p * N::T1P + u) + rg(g) + 4 * (l >> 5);
+          f[op * 64 + l] = i < N::OUT ? w2[(int64_t)i * N::H1 + k] : 0.0f;
+        }
+  }
+  float* bias = reinterpret_cast<float*>(blob.data() + N::BIAS_OFF);
+  memcpy(bias, b0, 4 * N::H0);
+  memcpy(bias + N::H0, b1, 4 * N::H1);
+  memcpy(bias + N::H0 + N::H1, b2, 4 * N::OUT);
+  return blob;
+}
+
 struct MlpKernel {
-  int in, h0, h1;
+  int in, h0, h1, precision;
   int64_t bytes;
   void (*fwd)(MlpArgs);
   std::vector<uint8_t> (*pack)(const float*, const float*, const float*, const float*, const float*, const float*);
@@ -392,7 +536,13 @@ struct MlpKernel {
 template <int IN, int H0, int H1, int CH, int PASSES>
 MlpKernel make_mlp() {
   using N = Net<IN, H0, H1, CH, PASSES>;
-  return MlpKernel{IN, H0, H1, N::BYTES, k_mlp<N>, pack<N>};
+  return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::BYTES, k_mlp<N>, pack<N>};
+}
+
+template <int IN, int H0, int H1, int PASSES>
+MlpKernel make_mlp_f32() {
+  using N = NetF<IN, H0, H1, PASSES>;
+  return MlpKernel{IN, H0, H1, WH_MLP_F32, N::BYTES, k_mlp_f32<N>, pack_f32<N>};
 }
 
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
@@ -401,10 +551,13 @@ const MlpKernel* find_mlp(const wh_mlp_desc* d) {
       make_mlp<37, 256, 256, 4, 2>(),     // Small:  obs 9*4+1,  [256, 256]
       make_mlp<82, 512, 512, 4, 4>(),     // Medium: obs 9*9+1,  [512, 512]
       make_mlp<145, 1024, 256, 2, 2>(),   // Large:  obs 9*16+1, [1024, 256]
+      make_mlp_f32<37, 256, 256, 1>(),    // the same shapes in exact f32
+      make_mlp_f32<82, 512, 512, 2>(),
+      make_mlp_f32<145, 1024, 256, 1>(),
   };
   if (!d || d->out_dim != 9) return nullptr;
   for (const auto& k : reg)
-    if (k.in == d->in_dim && k.h0 == d->hidden0 && k.h1 == d->hidden1) return &k;
+    if (k.in == d->in_dim && k.h0 == d->hidden0 && k.h1 == d->hidden1 && k.precision == d->precision) return &k;
   return nullptr;
 }
 
@@ -447,6 +600,11 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return WH_EHIP;
     cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  }
+  if (k->precision == WH_MLP_F32) {         // 32 rows per wave, 4 waves per workgroup
+    const int64_t ntask = (rows + 31) / 32;
+    hipLaunchKernelGGL(k->fwd, dim3((unsigned)((ntask + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
+    return hip_rc(hipGetLastError());
   }
   const int64_t ntask = (rows + MT / 2 - 1) / (MT / 2);
   const unsigned grid = (unsigned)(ntask < cus ? ntask : cus);

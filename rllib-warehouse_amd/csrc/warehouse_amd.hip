@@ -819,6 +819,54 @@ __device__ __forceinline__ void store_rewards(Lds<C>& L, const float (&rew)[C::N
   __builtin_amdgcn_wave_barrier();
 }
 
+// ----------------------------------------------------------------------------- assert mode
+// -DWH_CHECK builds verify SURVEY §5's invariants in the kernel after the state load and after
+// every step (and auto-reset): exactly R open requests (core.py:210-221 opens R, core.py:338-351
+// refills to R), every live agent inside the grid, every carried target a delivery cell
+// (core.py:177-188), every request byte a valid delivery index, the open-request mask equal to the
+// table, n <= agent slots.  Violations are counted in g_wh_check (read by wh_check_read): [0]
+// violations, [1] first failing env id, [2] its bit mask of failed checks, [3] env-states checked.
+#ifdef WH_CHECK
+__device__ unsigned long long g_wh_check[4];
+
+template <class C>
+__device__ __forceinline__ void check_env(const Regs<C>& s, const Lds<C>& L, int64_t e, int tid) {
+  const uint32_t n = (s.hdr >> 16) & 0xFFu;
+  uint32_t code = 0;
+  if (n > (uint32_t)C::NAM) code |= 1u;
+  if (__popcll(s.am) != C::R) code |= 2u;
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i) {
+    if ((uint32_t)i >= n) continue;
+    const uint32_t a = s.ag[i];
+    const uint32_t x = a & 0xFFu, y = (a >> 16) & 0xFFu, dx = (a >> 8) & 0xFFu, dy = a >> 24;
+    if (x >= (uint32_t)C::D || y >= (uint32_t)C::D) code |= 4u;
+    if ((dx == 0xFFu) != (dy == 0xFFu)) code |= 8u;
+    if (dx != 0xFFu) {
+      const bool xb = dx == 0u || dx == (uint32_t)(C::D - 1), yb = dy == 0u || dy == (uint32_t)(C::D - 1);
+      const bool ok = (xb && !yb && dy >= 2u && dy <= (uint32_t)(C::D - 3)) ||
+                      (yb && !xb && dx >= 2u && dx <= (uint32_t)(C::D - 3));
+      if (!ok) code |= 8u;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < C::P; ++j) {
+    const uint32_t tb = L.pkp[j][tid] & 0xFFu;
+    if ((tb != 0u) != (((s.am >> j) & 1ull) != 0ull)) code |= 16u;
+    if (tb > (uint32_t)C::DP) code |= 32u;
+  }
+  if (code) {
+    if (atomicAdd(&g_wh_check[0], 1ull) == 0ull) {
+      g_wh_check[1] = (unsigned long long)e;
+      g_wh_check[2] = code;
+    }
+  }
+}
+#define WH_CHECK_ENV(s, L, e, tid) check_env<C>(s, L, e, tid)
+#else
+#define WH_CHECK_ENV(s, L, e, tid) ((void)0)
+#endif
+
 struct StepParams {
   uint32_t* state;
   int64_t B;
@@ -928,6 +976,7 @@ __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
       }
     }
+    if (phase != PH_PRE) WH_CHECK_ENV(s, L, e, tid);
   }
   if (a.returns) a.returns[e] += ret;
   if (stats) a.stats.episode_return[e] = epr;
@@ -953,26 +1002,39 @@ __device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]
 template <class C, int POLICY>
 __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, Lds<C>& L, const Keys& k,
                                                uint32_t gid, int64_t e, int tid) {
+#ifdef WH_ABLATION
+  const int ablate = a.ablate;
+#else
+  constexpr int ablate = 0;
+#endif
   float* rrow = a.rewards + e * C::NAM;
   uint8_t* drow = a.dones + e;
   const int64_t rstride = a.B * C::NAM;
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t d[C::NAM];
-    policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+    if (ablate & 1) {
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
+    } else {
+      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+    }
     float rew[C::NAM];
     const bool done = step_env<C, false, false>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
-                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, 0);
-    store_row<C>(rrow, rew);
-    *drow = done ? 1 : 0;
+                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate);
+    if (!(ablate & 64)) {
+      store_row<C>(rrow, rew);
+      *drow = done ? 1 : 0;
+    }
     rrow += rstride;
     drow += a.B;
-    if (__any(done)) {           // wave-uniform test first: one branch on the common path
+    if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
       if (done) {
         reset_philox<C>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
       }
     }
+    WH_CHECK_ENV(s, L, e, tid);
   }
 }
 
@@ -991,6 +1053,10 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const uint32_t gid = (uint32_t)(a.env_offset + e);
   Regs<C> s;
   load_env_finish<C>(s, L, raw, (uint32_t)a.W, tid);
+#ifdef WH_CHECK
+  if (a.phase != PH_REGEN) WH_CHECK_ENV(s, L, e, tid);   // (a REGEN launch continues a PRE one)
+  atomicAdd(&g_wh_check[3], (unsigned long long)a.steps + 1ull);
+#endif
   // Drain the state loads here.  Their first uses are inside the step loop, so otherwise the
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
@@ -1045,6 +1111,7 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
   else
     reset_philox<C>(s, L, Keys{a.k0, a.k1}, (uint32_t)(a.env_offset + e), a.na, a.variable_n,
                     (uint32_t)a.W, tid);
+  if (!a.injected) WH_CHECK_ENV(s, L, e, tid);   // injected draws may legitimately be partial
   store_env<C>(s, L, a.state, a.B, e, a.na, tid);
 }
 
@@ -1509,7 +1576,34 @@ inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + BT - 1) / BT)); }
 // =============================================================================== C ABI
 extern "C" {
 
-const char* wh_version(void) { return "warehouse_amd gfx950 lane-per-env v2 " __DATE__; }
+const char* wh_version(void) {
+#ifdef WH_CHECK
+  return "warehouse_amd gfx950 lane-per-env v3 (assert mode) " __DATE__;
+#else
+  return "warehouse_amd gfx950 lane-per-env v3 " __DATE__;
+#endif
+}
+
+int wh_check_read(uint64_t* out, int32_t clear) {
+#ifdef WH_CHECK
+  if (!out) return WH_EINVAL;
+  unsigned long long v[4];
+  hipError_t he = hipDeviceSynchronize();
+  if (he == hipSuccess) he = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_wh_check), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (he != hipSuccess) return hip_err(he);
+  for (int i = 0; i < 4; ++i) out[i] = v[i];
+  if (clear) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    he = hipMemcpyToSymbol(HIP_SYMBOL(g_wh_check), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    if (he != hipSuccess) return hip_err(he);
+  }
+  return WH_OK;
+#else
+  (void)out;
+  (void)clear;
+  return WH_ENOTSUP;
+#endif
+}
 
 int wh_query(const wh_config* cfg, wh_layout* out) {
   Geometry g;
@@ -1607,7 +1701,7 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
   const uintptr_t ralign = (k->NAM % 4 == 0) ? 15u : 7u;
   if (k->step_fast[policy] && a.phase == PH_ALL && a.rewards && a.dones && !a.returns &&
       !a.stats.episode_return && !a.mask && !a.order && !a.regen && !a.n_inactive && a.autoreset &&
-      g.NA == k->NAM && ((uintptr_t)a.rewards & ralign) == 0 && a.ablate == 0)
+      g.NA == k->NAM && ((uintptr_t)a.rewards & ralign) == 0)
     kern = k->step_fast[policy];
   hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
   return hip_err(hipGetLastError());

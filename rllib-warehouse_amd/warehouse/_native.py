@@ -31,7 +31,8 @@ WH_POLICY_RANDOM = 2
 
 # every symbol include/warehouse_amd.h declares
 SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observe", "wh_policy",
-           "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version")
+           "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version",
+           "wh_check_read")
 
 
 class WhConfig(ctypes.Structure):
@@ -75,9 +76,13 @@ class WhEpisodeStats(ctypes.Structure):
     ]
 
 
+WH_MLP_BF16 = 0
+WH_MLP_F32 = 1
+
+
 class WhMlpDesc(ctypes.Structure):
     _fields_ = [("in_dim", ctypes.c_int32), ("hidden0", ctypes.c_int32), ("hidden1", ctypes.c_int32),
-                ("out_dim", ctypes.c_int32)]
+                ("out_dim", ctypes.c_int32), ("precision", ctypes.c_int32)]
 
 
 class WarehouseNativeError(RuntimeError):
@@ -117,6 +122,7 @@ def lib() -> ctypes.CDLL:
     L.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
     L.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
     L.wh_mlp_forward.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
+    L.wh_check_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), _I32]
     for name in SYMBOLS:
         if name != "wh_version":
             getattr(L, name).restype = ctypes.c_int

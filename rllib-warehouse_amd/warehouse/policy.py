@@ -1,13 +1,16 @@
 """The SAC policy network on the device (wh_mlp_forward): `trainer.compute_action(obs)` of
-scripts/rollout.py:84-86 for every agent row of a batch, so a trained-policy rollout stays on the
+scripts/rollout.py:72 for every agent row of a batch, so a trained-policy rollout stays on the
 GPU next to the simulator.
 
 Architecture = the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml:
 flat observation row (9R+1) -> Linear -> ReLU -> Linear -> ReLU -> Linear -> 9 action logits, hidden
 sizes [256,256] / [512,512] / [1024,256].  Weights come in torch nn.Linear layout ([out, in]); no
 checkpoint ships with the reference, so `MLPPolicy(variant)` initialises them like nn.Linear's
-default (U(-1/sqrt(fan_in), 1/sqrt(fan_in))) from a seed.  bf16 MFMA, f32 accumulation,
-activations rounded to bf16 between layers.
+default (U(-1/sqrt(fan_in), 1/sqrt(fan_in))) from a seed.
+
+precision="bf16" (default, fast): bf16 MFMA, f32 accumulation, activations rounded to bf16 between
+layers.  precision="f32": exact f32 on v_mfma_f32_32x32x2_f32 (an fmaf chain per output), i.e. the
+reference's TF fp32 policy up to summation order -- about 6x slower.
 """
 from __future__ import annotations
 
@@ -23,6 +26,7 @@ from .batched import require_device
 
 HIDDEN = {"small": (256, 256), "medium": (512, 512), "large": (1024, 256)}
 NUM_ACTIONS = 9
+PRECISIONS = {"bf16": nat.WH_MLP_BF16, "f32": nat.WH_MLP_F32}
 
 
 def init_weights(in_dim: int, hidden0: int, hidden1: int, seed: int = 0) -> Dict[str, np.ndarray]:
@@ -38,12 +42,15 @@ def init_weights(in_dim: int, hidden0: int, hidden1: int, seed: int = 0) -> Dict
 
 class MLPPolicy:
     def __init__(self, variant: str = "medium", weights: Optional[Dict[str, object]] = None, *,
-                 seed: int = 0, device=None):
+                 seed: int = 0, device=None, precision: str = "bf16"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         R = GEOMETRY[variant]["R"]
         self.in_dim = 9 * R + 1
         self.hidden = HIDDEN[variant]
+        self.precision = precision
         self.device = require_device(device)
-        self.desc = nat.WhMlpDesc(self.in_dim, self.hidden[0], self.hidden[1], NUM_ACTIONS)
+        self.desc = nat.WhMlpDesc(self.in_dim, self.hidden[0], self.hidden[1], NUM_ACTIONS, PRECISIONS[precision])
         nbytes = ctypes.c_int64()
         nat.check(nat.lib().wh_mlp_query(ctypes.byref(self.desc), ctypes.byref(nbytes)), "wh_mlp_query")
         if weights is None:

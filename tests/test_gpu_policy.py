@@ -8,6 +8,10 @@ Tolerances (stated here, checked below):
   * logits vs the plain fp32 network (no bf16 anywhere): |d| <= 3e-2 max|ref|  (the bf16 error).
   * argmax actions equal the reference's wherever its top-2 margin exceeds 1e-2.
   * explore=1 samples follow softmax(logits): chi-square over 9 bins below the 1e-4 quantile.
+  * precision="f32" (exact f32 MFMA): logits vs the float64 network (the reference policy is fp32)
+    |d| <= 1e-5 max|ref| per row (measured ~1e-7: f32 rounding in a different summation order), and
+    argmax equal to the float64 reference's on EVERY row whose top-2 margin exceeds 1e-5 max|ref|
+    (a closer pair is a tie at fp32 precision; the test reports how many such rows exist).
 """
 import numpy as np
 import pytest
@@ -108,7 +112,7 @@ def test_mlp_edge_cases(wh):
     _, lg = net(one, logits=True)
     ref = reference_logits(net.weights, np.zeros((1, net.in_dim), np.float32), bf16=True)
     np.testing.assert_allclose(lg.cpu().numpy(), ref, atol=2e-3, rtol=2e-3)
-    bad = nat.WhMlpDesc(net.in_dim, 128, 128, 9)
+    bad = nat.WhMlpDesc(net.in_dim, 128, 128, 9, 0)
     assert nat.lib().wh_mlp_forward(ctypes.byref(bad), net.packed.data_ptr(), 1, one.data_ptr(), None,
                                     None, 0, 0, 0, None) == nat.WH_ENOTSUP
 
@@ -147,3 +151,45 @@ def test_policy_rollout_transitions_vs_oracle(wh):
             ob.reset(L, S, d, mask=odone)
     np.testing.assert_array_equal(env.observe().cpu().numpy(), ob.observe(L, S))
     assert len({int(x) for x in np.unique(np.concatenate([a.reshape(-1) for a, _, _ in log]))}) > 1
+
+
+@pytest.mark.parametrize("variant,na", [("small", 4), ("medium", 8), ("large", 16)])
+def test_mlp_f32_matches_fp32_reference(wh, variant, na):
+    net = wh.policy.MLPPolicy(variant, seed=11, precision="f32")
+    x = observation_rows(wh, variant, na, 509, 3001)        # ragged row count, observation + random rows
+    acts, lg = net(x, logits=True)
+    lg, acts = lg.cpu().numpy().astype(np.float64), acts.cpu().numpy()
+    ref = reference_logits(net.weights, x.cpu().numpy(), bf16=False)          # float64 network
+    scale = np.abs(ref).max(axis=1, keepdims=True)
+    rel = np.abs(lg - ref) / scale
+    assert rel.max() <= 1e-5, rel.max()
+    srt = np.sort(ref, axis=1)
+    tie = (srt[:, -1] - srt[:, -2]) <= 1e-5 * scale[:, 0]
+    assert tie.sum() <= 2                                     # ties at fp32 precision are rare
+    np.testing.assert_array_equal(acts[~tie], ref.argmax(1)[~tie])
+    # and against torch's own float32 network on the same rows
+    import torch
+
+    t = {k: torch.as_tensor(v) for k, v in net.weights.items()}
+    xc = x.cpu()
+    h = torch.relu(xc @ t["w0"].T + t["b0"])
+    h = torch.relu(h @ t["w1"].T + t["b1"])
+    z32 = (h @ t["w2"].T + t["b2"]).numpy().astype(np.float64)
+    assert (np.abs(lg - z32) / scale).max() <= 1e-5
+    a2, _ = net(x)
+    np.testing.assert_array_equal(a2.cpu().numpy(), acts)
+
+
+def test_mlp_f32_edge_cases(wh):
+    import torch
+
+    net = wh.policy.MLPPolicy("medium", seed=5, precision="f32")
+    a, _ = net(torch.empty((0, net.in_dim), device=net.device))
+    assert a.numel() == 0
+    for rows in (1, 31, 33, 127):
+        x = torch.randn((rows, net.in_dim), device=net.device) * 4
+        _, lg = net(x, logits=True)
+        ref = reference_logits(net.weights, x.cpu().numpy(), bf16=False)
+        assert np.abs(lg.cpu().numpy() - ref).max() <= 1e-5 * np.abs(ref).max()
+    with pytest.raises(ValueError):
+        wh.policy.MLPPolicy("medium", precision="fp16")

@@ -90,12 +90,17 @@ def test_mlp_query_shapes():
     lib = _native.lib()
     n = ctypes.c_int64()
     for (i, h0, h1) in ((37, 256, 256), (82, 512, 512), (145, 1024, 256)):
-        d = _native.WhMlpDesc(i, h0, h1, 9)
+        d = _native.WhMlpDesc(i, h0, h1, 9, _native.WH_MLP_BF16)
         assert lib.wh_mlp_query(ctypes.byref(d), ctypes.byref(n)) == _native.WH_OK
         # bf16 weights (padded into MFMA operand order) + f32 biases
         assert n.value >= 2 * (i * h0 + h0 * h1 + 9 * h1) + 4 * (h0 + h1 + 9)
         assert n.value % 16 == 0 and n.value < 8 * (2 * (i * h0 + h0 * h1 + 32 * h1))
-    for bad in ((82, 512, 256, 9), (82, 512, 512, 4), (40, 256, 256, 9)):
+        d = _native.WhMlpDesc(i, h0, h1, 9, _native.WH_MLP_F32)
+        assert lib.wh_mlp_query(ctypes.byref(d), ctypes.byref(n)) == _native.WH_OK
+        # f32 weights in operand-stream order (layer 0 padded, recomputed per pass) + f32 biases
+        assert n.value >= 4 * (i * h0 + h0 * h1 + 9 * h1) + 4 * (h0 + h1 + 9)
+        assert n.value % 16 == 0 and n.value < 4 * (4 * (i + 32) * h0 + h0 * h1 + 32 * h1) + 4 * (h0 + h1 + 32) + 4096
+    for bad in ((82, 512, 256, 9, 0), (82, 512, 512, 4, 0), (40, 256, 256, 9, 0), (82, 512, 512, 9, 2)):
         d = _native.WhMlpDesc(*bad)
         assert lib.wh_mlp_query(ctypes.byref(d), ctypes.byref(n)) == _native.WH_ENOTSUP
     assert lib.wh_mlp_query(None, ctypes.byref(n)) == _native.WH_EINVAL
