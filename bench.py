@@ -11,6 +11,8 @@ nothing on the data path (no RCCL); a gloo group only aligns the timing window a
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
   alt_launch_mode -- the same workload as a hipGraph of one-step launches (state through HBM)
+  desync_episodes -- the headline launches after desynchronising the episodes (every step some
+                  envs of each wave end and reset), with its kernel time relative to the headline
   sampler_path -- the RLlib sampler route at the same B x NA: policy -> wh_vector_step (step +
                   auto-reset + float32 observation rows), with the observation kernel's roofline
                   (it writes B*NA*(9R+1)*4 bytes per step: HBM-write bound)
@@ -211,7 +213,7 @@ def launch_plan(K, chunk):
     return plan
 
 
-def measure(env, mode, policy, K, W, chunk, dev, world, dist):
+def measure(env, mode, policy, K, W, chunk, dev, world, dist, position=True):
     """Time K steps of `mode` (the contract's window).  The kernel time comes from HIP events recorded
     on the launch stream INSIDE that window around exactly the timed launches, so the roofline
     describes the launches that were timed.  Before the warmup, one untimed dry run of the same
@@ -269,7 +271,7 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist):
 
     timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)     # dry run (setup)
     pre += K
-    setup = window_setup_steps(T, K, pre + W)
+    setup = window_setup_steps(T, K, pre + W) if position else 0
     if setup:
         env.rollout(setup, policy, 0.0)           # position the window (untimed, no outputs)
     if W:
@@ -421,6 +423,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=200)
     ap.add_argument("--no-alt", action="store_true", help="skip the other launch mode")
     ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
+    ap.add_argument("--no-desync", action="store_true", help="skip the desynchronised-episodes measurement")
     ap.add_argument("--no-policy", action="store_true", help="skip the SAC-policy rollout measurement")
     ap.add_argument("--policy-steps", type=int, default=200)
     ap.add_argument("--policy-steps-f32", type=int, default=40)
@@ -456,6 +459,25 @@ def main():
                "steps_per_launch": m2["steps_per_launch"], "bytes_per_launch": m2["bytes_per_launch"],
                "roofline_frac": m2["achieved_gbs"] / HBM_PEAK_GBS, "host_fixed_us": m2["host_fixed_us"],
                "traffic": load_traffic(f"{args.variant}_n{NA}_{other}_k{m2['steps_per_launch']}")}
+
+    desync = None
+    if not args.no_desync and args.mode == "fused":
+        # episodes desynchronised like independent samplers (env e is 37e mod T steps ahead, so the 64
+        # lanes of a wave are spread over the episode): every step some lanes of most waves end, reset
+        # and run the expiry pass while the others do not
+        import numpy as np
+
+        env.reset()
+        T = int(env.geometry["T"])
+        env.stagger((np.arange(B, dtype=np.int64) * 37) % T)
+        md = measure(env, "fused", args.policy, K, W, args.chunk, dev, world, dist, position=False)
+        vd = aggregate_rate(world, B, NA, K, md["elapsed"])
+        desync = {"workload": "same launches after BatchedWarehouse.stagger: env e is 37e mod T steps ahead, so "
+                              "the lanes of every wave are spread over the episode and about B/T envs end "
+                              "their episode on every step",
+                  "value": vd, "ms_per_step": md["elapsed"] * 1e3 / K, "kernel_ms": md["kernel_ms"],
+                  "dones_in_window": md["dones_in_window"], "host_fixed_us": md["host_fixed_us"],
+                  "kernel_time_vs_synchronised": md["kernel_ms"] / m["kernel_ms"]}
 
     words = env.layout.words_per_env
     sampler = None
@@ -529,6 +551,7 @@ def main():
             },
             "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,
+            "desync_episodes": desync,
             "sampler_path": sampler,
             "policy_path": policy_line,
             "policy_path_f32": policy_f32,

@@ -170,6 +170,18 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream);
 
+/* A prepared wh_rollout: the same arguments resolved once (config validated, kernel and tables
+ * chosen) into an opaque handle, so a loop that launches the same rollout repeatedly pays one
+ * cheap call per launch (wh_launch_run enqueues exactly what wh_rollout would).  The buffers must
+ * stay valid while the handle is used; free it with wh_launch_free. */
+typedef struct wh_launch wh_launch;
+int wh_rollout_prepare(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy,
+                       float p, float* rewards, uint8_t* dones, float* returns, const wh_episode_stats* stats,
+                       int32_t autoreset, int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream,
+                       wh_launch** out);
+int wh_launch_run(const wh_launch* launch);
+void wh_launch_free(wh_launch* launch);
+
 /* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a
  * ReLU MLP, hidden_layer_sizes [256,256] Small / [512,512] Medium / [1024,256] Large, 9 action
  * logits), i.e. trainer.compute_action(obs) of scripts/rollout.py:72 for every agent row of a

@@ -1,6 +1,6 @@
 // policy_mlp.hip -- the SAC policy network forward on observation rows (bf16 MFMA, gfx950).
 //
-// What it replaces: `trainer.compute_action(obs)` of scripts/rollout.py:84-86 for the policy
+// What it replaces: `trainer.compute_action(obs)` of scripts/rollout.py:72 for the policy
 // model of scripts/experiments/warehouse-*-sac/*.yaml (policy_model: relu MLP, hidden_layer_sizes
 // [256,256] Small / [512,512] Medium / [1024,256] Large, 9 action logits), evaluated for every
 // agent row of a batch: explore = 0 -> argmax (compute_action(explore=False)), explore = 1 ->

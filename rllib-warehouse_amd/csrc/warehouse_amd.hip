@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <new>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1676,16 +1677,26 @@ int wh_reset(const wh_config* cfg, int64_t B, uint32_t* state, const uint8_t* ma
   return hip_err(hipGetLastError());
 }
 
-static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int policy,
-                       StepParams a, void* stream) {
+}  // extern "C"
+
+// A step launch with every argument resolved: what launch_step enqueues, and what a prepared
+// launch (wh_rollout_prepare / wh_launch_run) replays without re-validating anything.
+struct wh_launch {
+  void (*kern)(StepParams);
+  dim3 grid;
+  hipStream_t stream;
+  StepParams a;
+};
+
+static int resolve_step(const wh_config* cfg, int64_t B, uint32_t* state, int policy, StepParams a,
+                        void* stream, wh_launch* out) {
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
   int rc = prepare(cfg, B, stream, &g, &k, &tab);
   if (rc) return rc;
   if (policy < 0 || policy > 2) return WH_EINVAL;
-  if (B == 0) return WH_OK;
-  if (!state) return WH_EINVAL;
+  if (B > 0 && !state) return WH_EINVAL;
   a.state = state;
   a.B = B;
   a.na = g.NA;
@@ -1703,9 +1714,27 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
       !a.stats.episode_return && !a.mask && !a.order && !a.regen && !a.n_inactive && a.autoreset &&
       g.NA == k->NAM && ((uintptr_t)a.rewards & ralign) == 0)
     kern = k->step_fast[policy];
-  hipLaunchKernelGGL(kern, grid_for(B), dim3(BT), 0, (hipStream_t)stream, a);
+  out->kern = kern;
+  out->grid = grid_for(B);
+  out->stream = (hipStream_t)stream;
+  out->a = a;
+  return WH_OK;
+}
+
+static int enqueue(const wh_launch& l) {
+  if (l.a.B == 0) return WH_OK;
+  hipLaunchKernelGGL(l.kern, l.grid, dim3(BT), 0, l.stream, l.a);
   return hip_err(hipGetLastError());
 }
+
+static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int policy,
+                       StepParams a, void* stream) {
+  wh_launch l;
+  const int rc = resolve_step(cfg, B, state, policy, a, stream, &l);
+  return rc ? rc : enqueue(l);
+}
+
+extern "C" {
 
 int wh_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
             const int32_t* order, float* rewards, uint8_t* dones, const int32_t* regen,
@@ -1766,6 +1795,42 @@ int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, 
   a.variable_n = variable_n ? 1 : 0;
   return launch_step(cfg, B, state, policy, a, stream);
 }
+
+int wh_rollout_prepare(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy,
+                       float p, float* rewards, uint8_t* dones, float* returns, const wh_episode_stats* stats,
+                       int32_t autoreset, int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream,
+                       wh_launch** out) {
+  if (!out) return WH_EINVAL;
+  *out = nullptr;
+  if ((policy != WH_POLICY_GREEDY && policy != WH_POLICY_RANDOM) || steps < 0) return WH_EINVAL;
+  if (!(p >= 0.0f && p <= 1.0f) || !stats_ok(stats)) return WH_EINVAL;
+  StepParams a{};
+  if (stats) a.stats = *stats;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.returns = returns;
+  a.p = p;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = steps;
+  a.phase = PH_ALL;
+  a.autoreset = autoreset ? 1 : 0;
+  a.variable_n = variable_n ? 1 : 0;
+  wh_launch* l = new (std::nothrow) wh_launch;
+  if (!l) return WH_EINVAL;
+  const int rc = resolve_step(cfg, B, state, policy, a, stream, l);
+  if (rc) {
+    delete l;
+    return rc;
+  }
+  *out = l;
+  return WH_OK;
+}
+
+int wh_launch_run(const wh_launch* l) { return l ? enqueue(*l) : WH_EINVAL; }
+
+void wh_launch_free(wh_launch* l) { delete l; }
 
 int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* stream) {
   Geometry g;

@@ -17,6 +17,7 @@ trajectories those ids have in any other sharding (multi-GPU is a straight per-d
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -240,25 +241,41 @@ class BatchedWarehouse:
                    None if self.stats is None else self.stats.ref, int(bool(autoreset)),
                    int(self.train), self.seed, self.env_offset, self.stream)
 
+    def stagger(self, offsets, policy: str = "greedy", p: float = 0.0) -> None:
+        """Desynchronise episodes the way independent RLlib workers do: env e takes offsets[e]
+        extra steps (policy actions, auto-reset) while the others wait, via masked sampler steps
+        (wh_policy + wh_vector_step with an env mask).  Afterwards the envs' episode clocks differ, so
+        a fused rollout meets episode ends, resets and expiry passes on every step instead of all
+        at once.  Exactly the reference's per-env semantics: an env is only ever stepped or reset."""
+        off = torch.as_tensor(np.asarray(offsets) if not torch.is_tensor(offsets) else offsets)
+        off = off.to(device=self.device, dtype=torch.int32).reshape(self.B)
+        for s in range(int(off.max().item()) if self.B else 0):
+            self.vector_step(self.policy(policy, p), autoreset=True, observe=False, mask=off > s)
+
     def rollout_launcher(self, steps: int, policy: str = "greedy", p: float = 0.0, rewards=None,
                          dones=None, returns=None, autoreset: bool = True):
-        """rollout() with every argument bound once: returns a zero-argument callable that launches
-        the same fused rollout with no per-call argument handling (the tensors must stay alive and
-        in place while the callable is used)."""
+        """rollout() with every argument bound once (wh_rollout_prepare): returns a zero-argument
+        callable that launches the same fused rollout through one cheap wh_launch_run call (the
+        callable keeps the output tensors alive; the state tensor must stay in place)."""
         for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
                          (returns, (self.B,))):
             if t is not None and tuple(t.shape) != shape:
                 raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
-        fn = nat.lib().wh_rollout
-        args = (self._cfgp, self.B, self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
-                nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
-                None if self.stats is None else self.stats.ref, int(bool(autoreset)), int(self.train),
-                self.seed, self.env_offset, self.stream)
+        lib = nat.lib()
+        handle = ctypes.c_void_p()
+        nat.check(lib.wh_rollout_prepare(self._cfgp, self.B, self.state.data_ptr(), int(steps), POLICIES[policy],
+                                         float(p), nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
+                                         None if self.stats is None else self.stats.ref, int(bool(autoreset)),
+                                         int(self.train), self.seed, self.env_offset, self.stream,
+                                         ctypes.byref(handle)), "wh_rollout_prepare")
+        run, h = lib.wh_launch_run, handle.value
 
         def launch() -> None:
-            rc = fn(*args)
+            rc = run(h)
             if rc:
-                nat.check(rc, "wh_rollout")
+                nat.check(rc, "wh_launch_run")
+        launch.keep = (rewards, dones, returns, self.stats)      # buffers the handle points into
+        weakref.finalize(launch, lib.wh_launch_free, h)
         return launch
 
     # ------------------------------------------------------------------ canonical state

@@ -418,3 +418,25 @@ def test_max_size_batch_2m_envs(wh):
     acts = env.policy("greedy", 0.0)
     np.testing.assert_array_equal(acts[torch.as_tensor(ids, device=env.device)].cpu().numpy(),
                                   ob.greedy(L, S, 0.0, d))
+
+
+def test_prepared_launch_equals_rollout(wh):
+    """wh_rollout_prepare + wh_launch_run (BatchedWarehouse.rollout_launcher, bench.py's timed
+    launches) enqueue exactly wh_rollout: same rewards, dones and state after 3 launches."""
+    import torch
+
+    B, na, K = 2048, 8, 90
+    a = wh.BatchedWarehouse("medium", B, na, seed=31)
+    b = wh.BatchedWarehouse("medium", B, na, seed=31)
+    a.reset()
+    b.reset()
+    ra = torch.zeros((K, B, na), device=a.device)
+    rb = torch.zeros_like(ra)
+    da = torch.zeros((K, B), dtype=torch.uint8, device=a.device)
+    db = torch.zeros_like(da)
+    launch = b.rollout_launcher(K, "greedy", 0.0, rewards=rb, dones=db)
+    for _ in range(3):
+        a.rollout(K, "greedy", 0.0, rewards=ra, dones=da)
+        launch()
+        assert torch.equal(ra, rb) and torch.equal(da, db)
+    assert torch.equal(a.state, b.state)

@@ -179,3 +179,48 @@ def test_base_env_poll_send_try_reset(wh):
     assert ended == B
     with pytest.raises(IndexError):
         be.send_actions({0: {"0": 9}})
+
+
+@pytest.mark.parametrize("variant,na", [("medium", 8), ("large", 16)])
+def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na):
+    """Desynchronised episodes (BatchedWarehouse.stagger: env e takes e*7 % 200 extra masked greedy
+    steps), then a 260-step fused rollout: every step some envs end, reset and run the expiry pass
+    while their wave-mates do not.  Rewards and dones every step, and the final state, equal the
+    oracle's (philox draws, auto-reset per env)."""
+    import torch
+
+    B, seed, K = 1024, 13, 260
+    L = oc.layout_for(variant)
+    env = wh.BatchedWarehouse(variant, B, na, seed=seed)
+    env.reset()
+    S = ob.BState.zeros(L, B, na)
+    ids = np.arange(B)
+    ob.reset(L, S, ob.PhiloxDraws(seed, ids))
+    off = (ids * 7) % 200
+    env.stagger(off)
+    for s in range(int(off.max())):
+        idx = np.flatnonzero(off > s)
+        sub = take(S, idx)
+        d = ob.PhiloxDraws(seed, idx)
+        _, odone, _, _ = ob.step(L, sub, ob.greedy(L, sub, 0.0, d), d)
+        if odone.any():
+            ob.reset(L, sub, d, mask=odone)
+        put(S, idx, sub)
+    assert len(np.unique(S.t)) > 150                       # episode clocks are spread out
+    rew = torch.zeros((K, B, na), device=env.device)
+    dn = torch.zeros((K, B), dtype=torch.uint8, device=env.device)
+    env.rollout(K, "greedy", 0.0, rewards=rew, dones=dn)
+    d = ob.PhiloxDraws(seed, ids)
+    ends = 0
+    for s in range(K):
+        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        np.testing.assert_array_equal(rew[s].cpu().numpy(), orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
+        ends += int(odone.sum())
+        if odone.any():
+            ob.reset(L, S, d, mask=odone)
+    assert ends >= B                                        # every env crossed an episode end
+    c = {k: v.cpu().numpy() for k, v in env.to_canonical().items()}
+    np.testing.assert_array_equal(c["pos"], S.pos)
+    np.testing.assert_array_equal(c["pickup_target"], S.pk_tgt)
+    np.testing.assert_array_equal(c["t"], S.t)

@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "warehouse_amd.h")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(wh_[a-z_]+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(wh_[a-z_]+)\s*\(", text, flags=re.M)))
 
 
 def test_header_symbols_match_binding():

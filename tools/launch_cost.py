@@ -44,6 +44,14 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter(); x.add_(1); torch.cuda.synchronize(); r.append(time.perf_counter() - t0)
     print(f"tiny_op   {med(r):8.1f}")
+    r = []
+    for _ in range(50):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(s); x.add_(1); e1.record(s)
+        torch.cuda.synchronize()
+        r.append(e0.elapsed_time(e1) * 1e-3)
+    print(f"tiny_op_event {med(r):8.1f}")
     for K in (0, 1, 2, 5, 20, 200):
         rew = torch.zeros((K, B, NA), device=dev)
         dn = torch.zeros((K, B), dtype=torch.uint8, device=dev)
