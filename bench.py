@@ -261,6 +261,8 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist, position=True):
             o = off if whole else 0
             launches.append(env.rollout_launcher(c, policy, 0.0, rewards=rew[o:o + c], dones=dn[o:o + c]))
             off += c
+    # (events attached to the dispatch itself, wh_launch_run_timed, measured 7 us MORE window time per
+    # launch than these two marker records: tools/launch_cost.py)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run():

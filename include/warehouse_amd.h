@@ -180,6 +180,11 @@ int wh_rollout_prepare(const wh_config* cfg, int64_t B, uint32_t* state, int32_t
                        int32_t autoreset, int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream,
                        wh_launch** out);
 int wh_launch_run(const wh_launch* launch);
+/* wh_launch_run with HIP events (hipEvent_t, created by the caller with timing enabled) attached to
+ * the kernel dispatch itself (hipExtLaunchKernel): start/stop are stamped when the kernel starts and
+ * ends, so their span is the kernel's duration and no separate marker packets sit in the stream.
+ * Either event may be NULL (e.g. start on the first of several launches, stop on the last). */
+int wh_launch_run_timed(const wh_launch* launch, void* start_event, void* stop_event);
 void wh_launch_free(wh_launch* launch);
 
 /* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a

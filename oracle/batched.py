@@ -103,6 +103,21 @@ def _choose_without_replacement(avail_mask, count, words_fn, k_needed, first_wor
     return sel
 
 
+def _floyd_subset(P, R, words_fn, first_word, B, stride=2):
+    """Floyd's R-subset of range(P) as the philox contract draws it (word first + stride*j):
+    item j takes r = uniform_int(m+1) with m = P-R+j, or m when r is already taken."""
+    S = np.zeros(B, U64)
+    sel = np.zeros((B, R), np.int64)
+    for j in range(R):
+        m = P - R + j
+        r = ph.uniform_int(m + 1, words_fn(first_word + stride * j))
+        taken = ((S >> r.astype(U64)) & U64(1)).astype(bool)
+        s = np.where(taken, m, r)
+        S |= _bits(s)
+        sel[:, j] = s
+    return sel
+
+
 # --------------------------------------------------------------------------- reset
 def reset(L: Layout, S: BState, draws, mask: Optional[np.ndarray] = None, nmax: Optional[int] = None,
           n_fixed: Optional[int] = None) -> None:
@@ -120,10 +135,9 @@ def reset(L: Layout, S: BState, draws, mask: Optional[np.ndarray] = None, nmax: 
         spawn = np.zeros((B, NA, 2), np.int32)
         for i in range(NA):
             spawn[:, i] = valid[ph.uniform_int(len(valid), wf(1 + i))]
-        full_p = np.full(B, U64((1 << L.P) - 1 if L.P < 64 else 0xFFFFFFFFFFFFFFFF), U64)
         full_d = np.full(B, U64((1 << L.Dp) - 1 if L.Dp < 64 else 0xFFFFFFFFFFFFFFFF), U64)
         kR = np.full(B, L.R)
-        sel = _choose_without_replacement(full_p, L.P, wf, kR, 1 + NA)
+        sel = _floyd_subset(L.P, L.R, wf, 1 + NA, B)
         tgt = _choose_without_replacement(full_d, L.Dp, wf, kR, 2 + NA)
     else:
         n = np.asarray(draws.n if draws.n is not None else np.full(B, n_fixed or NA), np.int64)

@@ -15,7 +15,8 @@ include/warehouse_amd.h and DESIGN.md.
 Streams (purpose, t):
   RESET   (1, 0)      word 0: n = 1 + uniform_int(nmax, .) (Train variants only)
                       word 1+i: spawn cell of agent slot i = valid_cells[uniform_int(n_valid, .)]
-                      word 1+NA+2j: j-th request pickup = r-th not-yet-chosen pickup, r = uniform_int(P-j)
+                      word 1+NA+2j: j-th request pickup by Floyd's algorithm: m = P-R+j,
+                                    r = uniform_int(m+1); r unless already chosen, else m
                       word 2+NA+2j: its target = r-th not-yet-chosen delivery point, r = uniform_int(Dp-j)
   REGEN   (2, t_new)  word 2j (j<k): j-th reopened pickup = r-th remaining inactive, r = uniform_int(n_in-j)
                       word 2j+1: its target = r-th target not chosen in this regeneration, r = uniform_int(Dp-j)

@@ -19,6 +19,7 @@
 //    target bytes core.py:327-329), laid out [word][lane] so every lane hits its own bank, and no
 //    data-dependent branches: LDS side effects are predicated through neutral operands.
 //  * Counter-based Philox streams (no RNG state in HBM) or injected draws (parity mode).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -61,6 +62,7 @@ struct Cfg {
   static constexpr int NV = (D - 2) * (D - 2) - P;      // interior cells that are not pickups
   static constexpr TableLayout T = TableLayout(D, P, DP, NV);
   static constexpr int TBLW = T.bytes / 4;
+  static constexpr int TBL4 = (TBLW + 3) / 4;           // 16-byte chunks (device copy padded to them)
   static constexpr int L = 9 * R + 1;                    // observation row length
   static_assert(D <= 32, "positions are 5-bit fields (occupancy rows are 32-bit words)");
   static_assert(P <= 64 && DP <= 64, "bitmask sets hold at most 64 points");
@@ -215,7 +217,7 @@ struct Regs {
 
 template <class C>
 struct Lds {
-  alignas(16) uint32_t tbl[C::TBLW];
+  alignas(16) uint32_t tbl[4 * C::TBL4];
   uint32_t occ[C::D][BT];        // occupancy row y: bit x
   // Pickup point j of lane tid: low byte = request target + 1 (0 = none), high byte = expiry step
   // (low 8 bits).  Row P is scratch: predicated stores of lanes with nothing to write go there.
@@ -259,9 +261,21 @@ struct Lds {
   __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const { return tbl[C::T.dst / 4 - 1 + tb]; }
 };
 
+// Every 16-byte load of a lane is issued before its first LDS write, so the prologue pays one
+// memory round trip.  (A strided `for` loop over words compiled to load -> vmcnt(0) -> ds_write per
+// iteration: ~10 serial round trips per launch at Medium-8, most of a short launch's fixed cost.)
 template <class C>
 __device__ __forceinline__ void load_tables(uint32_t* dst, const uint32_t* __restrict__ tables) {
-  for (int w = threadIdx.x; w < C::TBLW; w += BT) dst[w] = tables[w];
+  constexpr int IT = (C::TBL4 + BT - 1) / BT;
+  const uint4* src = reinterpret_cast<const uint4*>(tables);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  uint4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+    if (C::TBL4 % BT == 0 || i + 1 < IT || (int)threadIdx.x + i * BT < C::TBL4) v[i] = src[threadIdx.x + i * BT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+    if (C::TBL4 % BT == 0 || i + 1 < IT || (int)threadIdx.x + i * BT < C::TBL4) d4[threadIdx.x + i * BT] = v[i];
 }
 
 template <class C>
@@ -346,17 +360,36 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 
 // ----------------------------------------------------------------------------- reset
 // core.py:167-221 (philox draws): spawn on interior non-pickup cells, open R requests.
-template <class C>
+// Law (the same as the reference's np.random.choice(P, R) paired with choice(Dp, R)): a uniform
+// R-subset of the pickup points, each given a distinct uniformly random delivery target.  The
+// subset comes from Floyd's algorithm (item j: r = uniform over [0, m] with m = P - R + j, take r
+// unless already taken, else m), one test and two ors per item; the targets are a uniform ordered
+// R-tuple without replacement (the r-th unused delivery point, r uniform over Dp - j), so pairing
+// them with the points in Floyd's order is a uniform injection.  NAC >= 0 is the agent count at
+// compile time (the fused rollout): every stream word then has a fixed place in the precomputed
+// Philox blocks, and the whole reset is straight-line code.
+template <class C, int NAC = -1>
 __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
-                                             int na, int variable_n, uint32_t W, int tid) {
+                                             int na_rt, int variable_n, uint32_t W, int tid) {
   const uint32_t ep = s.epi + 1u;
+  const int na = NAC >= 0 ? NAC : na_rt;
+  constexpr int NB = NAC >= 0 ? (1 + NAC + 2 * C::R + 3) / 4 : 1;
+  uint4 blk[NB];
+  if constexpr (NAC >= 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) blk[b] = stream_block(k, gid, ep, 0u, PUR_RESET, (uint32_t)b);
+  }
   Reader rd(k, gid, ep, 0u, PUR_RESET);
-  const uint32_t n = variable_n ? 1u + __umulhi(rd.word(0), (uint32_t)na) : (uint32_t)na;
+  auto word = [&](int j) -> uint32_t {
+    if constexpr (NAC >= 0) return comp(blk[j >> 2], j & 3);
+    else return rd.word(j);
+  };
+  const uint32_t n = variable_n ? 1u + __umulhi(word(0), (uint32_t)na) : (uint32_t)na;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) {
     uint32_t a = IDLE;
     if (i < na) {
-      const uint32_t v = __umulhi(rd.word(1 + i), (uint32_t)C::NV);
+      const uint32_t v = __umulhi(word(1 + i), (uint32_t)C::NV);
       const uint32_t cell = L.valid_cell(v);
       a = (i < (int)n) ? (cell | IDLE) : IDLE;
     }
@@ -365,17 +398,32 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
 #pragma unroll
   for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
   const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
-  uint64_t remP = low_mask<C::P>(), remD = low_mask<C::DP>();
+  uint32_t plo = 0, phi = 0;                // Floyd's subset so far
+  uint64_t remD = low_mask<C::DP>();
+  uint32_t t0 = 0;
+#pragma unroll
   for (int j = 0; j < C::R; ++j) {
-    const uint32_t r1 = __umulhi(rd.word(1 + na + 2 * j), (uint32_t)(C::P - j));
-    const int sel = select_bit64(remP, r1);
-    remP &= ~(1ull << sel);
-    const uint32_t r2 = __umulhi(rd.word(2 + na + 2 * j), (uint32_t)(C::DP - j));
-    const int tg = select_bit64(remD, r2);
+    constexpr int M0 = C::P - C::R;
+    const uint32_t m = (uint32_t)(M0 + j);
+    const uint32_t r = __umulhi(word(1 + na + 2 * j), m + 1u);
+    uint32_t sel = r;
+    if (j > 0) {   // taken already: bit r of the subset, moved to bit 63 by one 64-bit shift
+      const uint64_t sh = (((uint64_t)phi << 32) | plo) << (63u - r);
+      sel = msel(sgn((uint32_t)(sh >> 32)), m, r);
+    }
+    const uint64_t sb = 1ull << sel;
+    plo |= (uint32_t)sb;
+    phi |= (uint32_t)(sb >> 32);
+    const uint32_t r2 = __umulhi(word(2 + na + 2 * j), (uint32_t)(C::DP - j));
+    uint32_t tg;
+    if (j == 0) tg = r2;
+    else if (j == 1) tg = r2 + ((t0 - 1u - r2) >> 31);   // + (r2 >= first): skip it
+    else tg = select_bit64(remD, r2);
+    if (j == 0) t0 = r2;
     remD &= ~(1ull << tg);
-    L.pkp[sel][tid] = (uint16_t)((uint32_t)(tg + 1) | wexp);
+    L.pkp[sel][tid] = (uint16_t)((tg + 1u) | wexp);
   }
-  s.am = low_mask<C::P>() & ~remP;
+  s.am = ((uint64_t)phi << 32) | plo;
   s.hdr = (n << 16) | (1u << 24);
   s.epi = ep;
 }
@@ -524,15 +572,41 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     //      which lets its lookups be issued inside it.
     WH_PHASE_MARK(expire);
     if (!(ablate & 4) && __any(t >= s.wskip)) {
-      uint64_t expired = 0;
+      if (__any(__popcll(s.am) > C::R)) {   // a hand-built state with more than R requests: scan all
+        uint64_t expired = 0;
 #pragma unroll
-      for (int j = 0; j < C::P; ++j) {
-        const uint32_t v = L.pkp[j][tid];
-        const bool ex = (v & 0xFFu) != 0u && (v >> 8) == (t & 0xFFu);
-        if (ex) L.clear_target(j, tid);
-        expired |= (uint64_t)ex << j;
+        for (int j = 0; j < C::P; ++j) {
+          const uint32_t v = L.pkp[j][tid];
+          const bool ex = (v & 0xFFu) != 0u && (v >> 8) == (t & 0xFFu);
+          if (ex) L.clear_target(j, tid);
+          expired |= (uint64_t)ex << j;
+        }
+        s.am &= ~expired;
+      } else {
+        // walk the (at most R) open requests in the mask, as the policy does; index P (missing
+        // slots) is the scratch row, and its "expiry" is discarded by the j < P test
+        uint32_t mlo = (uint32_t)s.am, mhi = (uint32_t)(s.am >> 32), elo = 0, ehi = 0;
+        const uint32_t t8 = t & 0xFFu;
+#pragma unroll
+        for (int r = 0; r < C::R; ++r) {
+          uint32_t flo, fhi;
+          asm("v_ffbl_b32 %0, %1" : "=v"(flo) : "v"(mlo));   // 0xFFFFFFFF when empty
+          asm("v_ffbl_b32 %0, %1" : "=v"(fhi) : "v"(mhi));
+          const uint32_t j = __builtin_elementwise_min(
+              __builtin_elementwise_min(flo, __builtin_elementwise_add_sat(fhi, 32u)), (uint32_t)C::P);
+          const uint32_t v = L.pkp[j][tid];
+          const uint32_t ex = bop3<TA & TB>(mask_z((v >> 8) ^ t8), sgn(j - (uint32_t)C::P), 0xFFFFFFFFu);
+          *reinterpret_cast<uint8_t*>(&L.pkp[msel(ex, j, (uint32_t)C::P)][tid]) = 0;
+          const uint64_t b = 1ull << (j & 63u);
+          elo |= bop3<TA & TB>(ex, (uint32_t)b, 0u);
+          ehi |= bop3<TA & TB>(ex, (uint32_t)(b >> 32), 0u);
+          uint64_t m = ((uint64_t)mhi << 32) | mlo;
+          m &= m - 1ull;
+          mlo = (uint32_t)m;
+          mhi = (uint32_t)(m >> 32);
+        }
+        s.am &= ~(((uint64_t)ehi << 32) | elo);
       }
-      s.am &= ~expired;
     }
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
@@ -1030,7 +1104,7 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
     drow += a.B;
     if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
       if (done) {
-        reset_philox<C>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+        reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
       }
@@ -1045,8 +1119,9 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const int tid = threadIdx.x;
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
   const bool live = e < a.B && (FAST || !a.mask || a.mask[e]);
+  const int na = FAST ? C::NAM : a.na;   // the fast instance runs na == NAM only (resolve_step)
   RawEnv<C> raw;
-  if (live) load_env_issue<C>(raw, a.state, a.B, e, a.na);
+  if (live) load_env_issue<C>(raw, a.state, a.B, e, na);
   load_tables<C>(L.tbl, a.tables);
   __syncthreads();
   if (!live) return;
@@ -1081,7 +1156,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
-  store_env<C>(s, L, a.state, a.B, e, a.na, tid);
+  store_env<C>(s, L, a.state, a.B, e, na, tid);
 }
 
 struct ResetParams {
@@ -1487,7 +1562,9 @@ int device_tables(const Geometry& g, int expect_words, hipStream_t stream, const
   if (he != hipSuccess) return hip_err(he);
   if (cur != dev && (he = hipSetDevice(dev)) != hipSuccess) return hip_err(he);
   uint32_t* d = nullptr;
-  he = hipMalloc(&d, w.size() * 4);
+  const size_t padded = (w.size() + 3) / 4 * 16;   // load_tables reads whole 16-byte chunks
+  he = hipMalloc(&d, padded);
+  if (he == hipSuccess) he = hipMemset(d, 0, padded);
   if (he == hipSuccess) he = hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice);
   if (cur != dev) (void)hipSetDevice(cur);
   if (he != hipSuccess) return hip_err(he);
@@ -1829,6 +1906,15 @@ int wh_rollout_prepare(const wh_config* cfg, int64_t B, uint32_t* state, int32_t
 }
 
 int wh_launch_run(const wh_launch* l) { return l ? enqueue(*l) : WH_EINVAL; }
+
+int wh_launch_run_timed(const wh_launch* l, void* start_event, void* stop_event) {
+  if (!l) return WH_EINVAL;
+  if (l->a.B == 0) return WH_OK;
+  StepParams a = l->a;
+  void* args[] = {&a};
+  return hip_err(hipExtLaunchKernel(reinterpret_cast<const void*>(l->kern), l->grid, dim3(BT), args, 0,
+                                    l->stream, (hipEvent_t)start_event, (hipEvent_t)stop_event, 0));
+}
 
 void wh_launch_free(wh_launch* l) { delete l; }
 

@@ -32,7 +32,7 @@ WH_POLICY_RANDOM = 2
 # every symbol include/warehouse_amd.h declares
 SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observe", "wh_policy",
            "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version",
-           "wh_check_read", "wh_rollout_prepare", "wh_launch_run", "wh_launch_free")
+           "wh_check_read", "wh_rollout_prepare", "wh_launch_run", "wh_launch_run_timed", "wh_launch_free")
 
 
 class WhConfig(ctypes.Structure):
@@ -126,6 +126,7 @@ def lib() -> ctypes.CDLL:
     L.wh_rollout_prepare.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P,
                                      ctypes.POINTER(ctypes.c_void_p)]
     L.wh_launch_run.argtypes = [_P]
+    L.wh_launch_run_timed.argtypes = [_P, _P, _P]
     L.wh_launch_free.argtypes = [_P]
     L.wh_launch_free.restype = None
     for name in SYMBOLS:

@@ -253,10 +253,13 @@ class BatchedWarehouse:
             self.vector_step(self.policy(policy, p), autoreset=True, observe=False, mask=off > s)
 
     def rollout_launcher(self, steps: int, policy: str = "greedy", p: float = 0.0, rewards=None,
-                         dones=None, returns=None, autoreset: bool = True):
+                         dones=None, returns=None, autoreset: bool = True, events=None):
         """rollout() with every argument bound once (wh_rollout_prepare): returns a zero-argument
         callable that launches the same fused rollout through one cheap wh_launch_run call (the
-        callable keeps the output tensors alive; the state tensor must stay in place)."""
+        callable keeps the output tensors alive; the state tensor must stay in place).
+        events=(start, stop) (torch.cuda.Event with enable_timing=True, either may be None): every
+        launch stamps them at the kernel's own start and end (wh_launch_run_timed), so
+        start.elapsed_time(stop) is the kernel's duration, with no marker packets around it."""
         for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
                          (returns, (self.B,))):
             if t is not None and tuple(t.shape) != shape:
@@ -268,13 +271,29 @@ class BatchedWarehouse:
                                          None if self.stats is None else self.stats.ref, int(bool(autoreset)),
                                          int(self.train), self.seed, self.env_offset, self.stream,
                                          ctypes.byref(handle)), "wh_rollout_prepare")
-        run, h = lib.wh_launch_run, handle.value
+        h = handle.value
+        if events is None:
+            run = lib.wh_launch_run
 
-        def launch() -> None:
-            rc = run(h)
-            if rc:
-                nat.check(rc, "wh_launch_run")
-        launch.keep = (rewards, dones, returns, self.stats)      # buffers the handle points into
+            def launch() -> None:
+                rc = run(h)
+                if rc:
+                    nat.check(rc, "wh_launch_run")
+        else:
+            run = lib.wh_launch_run_timed
+            s = torch.cuda.current_stream(self.device)
+            for ev in events:        # torch creates the HIP event at its first record
+                if ev is not None:
+                    ev.record(s)
+            e0, e1 = (ctypes.c_void_p(None if ev is None else int(ev.cuda_event)) for ev in events)
+            if any(ev is not None and not c.value for ev, c in zip(events, (e0, e1))):
+                raise RuntimeError("rollout_launcher: an event has no HIP event handle")
+
+            def launch() -> None:
+                rc = run(h, e0, e1)
+                if rc:
+                    nat.check(rc, "wh_launch_run_timed")
+        launch.keep = (rewards, dones, returns, self.stats, events)   # buffers the handle points into
         weakref.finalize(launch, lib.wh_launch_free, h)
         return launch
 

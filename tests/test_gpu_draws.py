@@ -72,6 +72,27 @@ def test_device_reset_law(wh):
     assert chi2_uniform(np.bincount(tg.ravel(), minlength=L.Dp)) > ALPHA
 
 
+def test_device_reset_subset_law(wh):
+    """Reset requests (Small, P=16, R=4): all C(16,4) subsets equally likely (Floyd's algorithm on
+    the device is the law of choice(P, R, replace=False)), and the target of the lowest open point
+    uniform over the delivery points (pairing with a uniform ordered target tuple)."""
+    from math import comb
+
+    B = 65536
+    env = wh.BatchedWarehouse("small", B, 4, seed=123)
+    env.reset()
+    c = canon(env)
+    L = oc.layout_for("small")
+    open_ = c["pickup_target"] > -1
+    assert (open_.sum(1) == L.R).all()
+    code = (open_.astype(np.int64) << np.arange(L.P)).sum(1)
+    counts = np.unique(code, return_counts=True)[1]
+    assert len(counts) == comb(L.P, L.R)
+    assert chi2_uniform(counts) > ALPHA
+    first = c["pickup_target"][np.arange(B), open_.argmax(1)]
+    assert chi2_uniform(np.bincount(first, minlength=L.Dp)) > ALPHA
+
+
 def _regen_state(wh, k, B, seed):
     """B copies of one Medium state (one idle agent far from every pickup, staying put) with R-k open
     requests, so the next step's only random event is regeneration of exactly k requests."""

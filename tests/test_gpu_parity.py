@@ -440,3 +440,32 @@ def test_prepared_launch_equals_rollout(wh):
         launch()
         assert torch.equal(ra, rb) and torch.equal(da, db)
     assert torch.equal(a.state, b.state)
+
+
+def test_timed_launch_equals_rollout_and_stamps_events(wh):
+    """wh_launch_run_timed (events attached to the dispatch, bench.py's fused window) enqueues exactly
+    wh_rollout, and its start/stop events bracket the kernel: a positive span that grows with K."""
+    import torch
+
+    B, na = 4096, 8
+    spans = {}
+    for K in (5, 60):
+        a = wh.BatchedWarehouse("medium", B, na, seed=37)
+        b = wh.BatchedWarehouse("medium", B, na, seed=37)
+        a.reset()
+        b.reset()
+        ra = torch.zeros((K, B, na), device=a.device)
+        rb = torch.zeros_like(ra)
+        da = torch.zeros((K, B), dtype=torch.uint8, device=a.device)
+        db = torch.zeros_like(da)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        launch = b.rollout_launcher(K, "greedy", 0.0, rewards=rb, dones=db, events=(e0, e1))
+        for _ in range(4):
+            a.rollout(K, "greedy", 0.0, rewards=ra, dones=da)
+            launch()
+            torch.cuda.synchronize()
+            assert torch.equal(ra, rb) and torch.equal(da, db)
+        assert torch.equal(a.state, b.state)
+        spans[K] = e0.elapsed_time(e1)
+        assert spans[K] > 0.0
+    assert spans[60] > spans[5]

@@ -174,3 +174,27 @@ def test_philox_reset_distribution():
     nc = np.bincount(S.n, minlength=10)[1:]
     assert (np.abs(nc - B / 9) < 6 * np.sqrt(B / 9)).all()
     assert ((S.pk_tgt > -1).sum(1) == L.R).all()
+
+
+def test_philox_reset_subset_and_pairing_law():
+    """The philox reset's request law (Floyd subset + ordered targets) equals the reference's
+    choice(P, R, replace=False) paired with choice(Dp, R, replace=False): every R-subset of pickup
+    points equally likely, and the lowest open point's target uniform over the delivery points."""
+    from math import comb
+
+    from scipy import stats
+
+    L = oc.layout_for("small")
+    B = 60000
+    S = ob.BState.zeros(L, B, 4)
+    ob.reset(L, S, ob.PhiloxDraws(11, np.arange(B)))
+    open_ = S.pk_tgt > -1
+    assert (open_.sum(1) == L.R).all()
+    code = (open_.astype(np.int64) << np.arange(L.P)).sum(1)
+    counts = np.unique(code, return_counts=True)[1]
+    assert len(counts) == comb(L.P, L.R)
+    exp = B / comb(L.P, L.R)
+    assert stats.chi2.sf(((counts - exp) ** 2 / exp).sum(), len(counts) - 1) > 1e-6
+    first = S.pk_tgt[np.arange(B), open_.argmax(1)]
+    c = np.bincount(first, minlength=L.Dp)
+    assert stats.chi2.sf(((c - B / L.Dp) ** 2 / (B / L.Dp)).sum(), L.Dp - 1) > 1e-6

@@ -8,6 +8,8 @@ Prints medians (us) over repetitions:
   call_K         the bound wh_rollout call alone (host time, no sync)
   wall_K         call + sync (what bench.py's window sees for one launch of K steps)
   event_K        HIP-event span around the launch on its stream
+  plain_K        wall of the launch + sync with no events at all
+  ext_K          wall / span with the events attached to the dispatch (wh_launch_run_timed)
 """
 import os
 import statistics
@@ -52,7 +54,8 @@ def main():
         torch.cuda.synchronize()
         r.append(e0.elapsed_time(e1) * 1e-3)
     print(f"tiny_op_event {med(r):8.1f}")
-    for K in (0, 1, 2, 5, 20, 200):
+    Ks = (20,) if "--quick" in sys.argv else (0, 1, 2, 5, 20, 200)
+    for K in Ks:
         rew = torch.zeros((K, B, NA), device=dev)
         dn = torch.zeros((K, B), dtype=torch.uint8, device=dev)
         launch = env.rollout_launcher(K, "greedy", 0.0, rewards=rew, dones=dn)
@@ -73,6 +76,27 @@ def main():
             call.append(t1 - t0); wall.append(t2 - t0); span.append(e0.elapsed_time(e1) * 1e-3)
         print(f"K={K:4d} call {med(call):8.1f}  wall {med(wall):8.1f}  event {med(span):8.1f}  "
               f"wall-event {med(wall) - med(span):7.1f}  event/step {med(span) / max(K, 1):7.2f}")
+        plain = []
+        for _ in range(30):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            launch()
+            torch.cuda.synchronize()
+            plain.append(time.perf_counter() - t0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tl = env.rollout_launcher(K, "greedy", 0.0, rewards=rew, dones=dn, events=(e0, e1))
+        tl()
+        torch.cuda.synchronize()
+        wall, span = [], []
+        for _ in range(30):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tl()
+            torch.cuda.synchronize()
+            wall.append(time.perf_counter() - t0)
+            span.append(e0.elapsed_time(e1) * 1e-3)
+        print(f"K={K:4d} plain wall {med(plain):8.1f}  ext wall {med(wall):8.1f}  ext span {med(span):8.1f}  "
+              f"wall-span {med(wall) - med(span):7.1f}")
 
 
 if __name__ == "__main__":
