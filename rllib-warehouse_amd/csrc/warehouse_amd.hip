@@ -40,6 +40,11 @@ constexpr uint32_t ROWB = 2 * BT;   // bytes per pickup-point row of the LDS pic
 enum Policy { POL_EXTERNAL = 0, POL_GREEDY = 1, POL_RANDOM = 2 };
 enum Purpose : uint32_t { PUR_RESET = 1, PUR_REGEN = 2, PUR_POLICY = 3, PUR_RANDOM = 4 };
 constexpr int PH_ALL = 0, PH_PRE = 1, PH_REGEN = 2, PH_POLICY = 3;
+#ifdef WH_ABLATION
+constexpr bool kAblationBuild = true;    // ablation moves are arbitrary: keep the off-grid clamp
+#else
+constexpr bool kAblationBuild = false;
+#endif
 
 constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle agent
 constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
@@ -466,7 +471,10 @@ __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e,
 // after reset), else for the nearest open request by Manhattan distance, first (lowest pickup
 // index) minimum wins; step = clip(goal - pos, -1, 1).  Random actions come from the
 // POLICY/RANDOM streams.  Slots >= n get arbitrary steps: step_env never moves them.
-template <class C, int POLICY>
+// EFF: random moves are returned as the step they take (off-grid coordinates kept, core.py:282-287),
+// so a step loop can add them without the clamp (step_env<CLAMP = false>); wh_policy reports the
+// drawn action itself (EFF = false), as solvers.py:44-45 returns action_space.sample().
+template <class C, int POLICY, bool EFF = false>
 __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, const Keys& k,
                                              uint32_t gid, float p, uint32_t (&d)[C::NAM]) {
   const uint32_t t = s.hdr & 0xFFFFu;
@@ -512,12 +520,13 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       const uint32_t pos = a & XY16;
       uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-      for (int r = 0; r < C::R; ++r)   // key = dist << 16 | pickup << 10 | x << 5 | y
+      for (int r = 0; r < C::R; ++r)   // key = dist << 16 | pickup << 10 | y << 5 | x
         best = min(best, __builtin_amdgcn_sad_hi_u8(pos, rp[r], tg[r]));
-      const uint32_t near = (((best >> 5) & 31u) | (best << 16)) & 0x001F001Fu;   // tag (x, y) -> x | y << 16
-      const uint32_t dst = (a >> 8) & XY16;
+      const uint32_t near = (__builtin_amdgcn_ubfe(best, 5u, 5u) << 16) | (best & 31u);   // y << 16 | x
+      const uint32_t dst = __builtin_amdgcn_perm(a, a, 0x0C030C01u);   // target bytes 1, 3 -> x | y << 16
       const uint32_t idle = (uint32_t)__builtin_amdgcn_sbfe((int)a, 15, 1);   // target byte 0xFF
       const uint32_t goal = msel(idle, near, dst);
+      // goal is a grid cell, so pos + d stays on the grid: step_env<CLAMP = false> adds it as is
       d[i] = pk_min_i16(pk_max_i16(pk_sub_i16(goal, pos), 0xFFFFFFFFu), 0x00010001u);
     }
     if (p > 0.0f) {
@@ -529,7 +538,11 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
           const int i = 2 * b + h;
           if (i < C::NAM) {
             const float u = (float)(comp(blk, 2 * h) >> 8) * (1.0f / 16777216.0f);
-            const uint32_t rnd = L.mv(__umulhi(comp(blk, 2 * h + 1), 9u));
+            uint32_t rnd = L.mv(__umulhi(comp(blk, 2 * h + 1), 9u));
+            if (EFF) {
+              const uint32_t pos = s.ag[i] & XY16;
+              rnd = pk_sub_i16(step16<C::D>(pos, rnd), pos);
+            }
             d[i] = (u < p) ? rnd : d[i];
           }
         }
@@ -545,7 +558,9 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
 // so each phase is one basic block and its LDS reads issue back to back.
 // INJ = false compiles the injected-draw regeneration out (the fused rollout and the sampler step
 // always draw from philox): less code in the step loop and no per-step test of `regen`.
-template <class C, bool ORDERED, bool INJ = true>
+// CLAMP = false: the steps come from the greedy policy, whose goals are grid cells, so pos + d
+// never leaves the grid and the off-grid rule (a clamp) is the identity.
+template <class C, bool ORDERED, bool INJ = true, bool CLAMP = true>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
                                          const int32_t* __restrict__ actions_g,
@@ -672,7 +687,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) {
           pp[i] = s.ag[i] & XY16;
-          cc[i] = step16<C::D>(pp[i], dstep[i]);
+          cc[i] = CLAMP ? step16<C::D>(pp[i], dstep[i]) : as_u(as_s2(pp[i]) + as_s2(dstep[i]));
         }
         // Predicates are kept in bit 31 of VGPRs (x31 names) and selects are v_bitop3 with
         // 0 / all-ones masks (m names): no VCC round trips on the serial chain.
@@ -696,7 +711,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           // exactly "same square, opposite diagonal", i.e. square key == i's with the top byte
           // flipped (^ 0xFC000000), which no straight move's key ever equals.
           const uint32_t key = p | (c << 8);
-          const uint32_t dd = pk_sub_i16(c, p);
+          const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
           const int ddot = __builtin_amdgcn_sdot2(as_s2(dd), as_s2(__builtin_amdgcn_alignbit(dd, dd, 16)), 0, false);
           const uint32_t ukey = pk_min_u16(p, c) + ((uint32_t)ddot << 24);
           uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
@@ -1024,10 +1039,10 @@ __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
     } else {
-      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+      policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C, ORDERED>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, phase,
+    const bool done = step_env<C, ORDERED, true, POLICY != POL_GREEDY || kAblationBuild>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, phase,
                                   (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, ablate);
     if (phase != PH_REGEN) {
       if (a.rewards && !(ablate & 64))
@@ -1091,10 +1106,10 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
     } else {
-      policy_steps<C, POLICY>(s, L, k, gid, a.p, d);
+      policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C, false, false>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
                                                 (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate);
     if (!(ablate & 64)) {
       store_row<C>(rrow, rew);
@@ -1493,7 +1508,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   std::vector<uint16_t> cell(256 * D, 0);
   std::vector<uint32_t> rp(g.P + 1), tag(g.P + 1);
   rp[g.P] = 0x00FF00FFu;
-  tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);
+  tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);   // pickup << 10 | y << 5 | x
   for (int ix = 0; ix < g.NR; ++ix)
     for (int iy = 0; iy < g.NR; ++iy)
       for (int q = 0; q < 4; ++q) {
@@ -1503,7 +1518,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
         if (cell[ci]) *bad = 1;  // overlapping racks
         cell[ci] = (uint16_t)((j + 1) * ROWB);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
-        tag[j] = ((uint32_t)j << 10) | ((uint32_t)x << 5) | (uint32_t)y;
+        tag[j] = ((uint32_t)j << 10) | ((uint32_t)y << 5) | (uint32_t)x;
       }
   std::vector<uint32_t> dst(g.DP);
   for (int d = 0; d < g.DP; ++d) {
