@@ -187,6 +187,15 @@ __device__ __forceinline__ uint32_t pk_sub_i16(uint32_t a, uint32_t b) {
   return r;
 }
 
+// dx * dy of a packed (dx, dy) i16 pair in ONE op, in both halves: v_pk_mul_lo_u16 of the pair with
+// itself, the second operand's halves swapped by op_sel (a builtin dot2 costs a v_alignbit and a
+// zeroed accumulator on top).
+__device__ __forceinline__ uint32_t mul_swap(uint32_t d) {
+  uint32_t r;
+  asm("v_pk_mul_lo_u16 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(d));
+  return r;
+}
+
 // clamp(p + d) per 16-bit lane: the reference keeps the old coordinate when a +-1 move leaves
 // [0, D) (core.py:284-287), which for unit moves is exactly a clamp to [0, D-1].
 template <int D>
@@ -706,14 +715,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
           // forbidden moves (core.py:293-297): the reverse of every accepted move, matched as an
           // ordered (from, to) key, and for accepted diagonals the two crossing moves.  A move's
-          // square key is the low corner of the 2x2 square it spans plus 2*dx*dy in the top byte
-          // (+2 one diagonal, -2 the other, 0 straight or stay); "either crossing move of i" is
+          // square key is the low corner of the 2x2 square it spans plus dx*dy in the top byte
+          // (0x01 one diagonal, 0xFF the other, 0 straight or stay); "either crossing move of i" is
           // exactly "same square, opposite diagonal", i.e. square key == i's with the top byte
-          // flipped (^ 0xFC000000), which no straight move's key ever equals.
+          // flipped (^ 0xFE000000: 0x01 <-> 0xFF), which no straight move's key (0) ever equals.
           const uint32_t key = p | (c << 8);
           const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
-          const int ddot = __builtin_amdgcn_sdot2(as_s2(dd), as_s2(__builtin_amdgcn_alignbit(dd, dd, 16)), 0, false);
-          const uint32_t ukey = pk_min_u16(p, c) + ((uint32_t)ddot << 24);
+          const uint32_t ukey = pk_min_u16(p, c) + (mul_swap(dd) << 24);   // top byte dx*dy: 1, 0xFF, 0
           uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
 #pragma unroll
           for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
@@ -723,7 +731,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           atomicOr(&L.occ[c >> 16][tid], bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
           const uint32_t dxy = c ^ p;
           rk[sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
-          xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFC000000u);
+          xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
           const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
           s.ag[sidx] = moved;
           mokp = mok;
