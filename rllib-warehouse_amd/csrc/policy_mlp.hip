@@ -41,35 +41,46 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int MT = 512;                 // threads per workgroup: 8 waves x 32 samples (2 per SIMD)
 constexpr uint32_t PUR_MLP = 5;         // philox purpose (1-4 are the simulator's, philox.h)
 
-template <int IN_, int H0_, int H1_, int CH_, int PASSES_>
+// One launch shape per network; every layer runs exactly once per sample.  A wave computes 32
+// samples (the MFMA tile's columns); WAVES waves per workgroup share every staged weight operand,
+// which streams through two LDS stages in consumption order.  Two dataflows, by which layer's
+// activations fit the registers:
+//  MODE 0 (H0 <= 512): layer 0 first, all H0 hidden units kept as bf16 B-operand fragments (T0 x 8
+//    VGPRs); then layer 1 row tile by row tile with K = H0 at hand, each tile's bias + ReLU
+//    feeding its two layer-2 MFMAs at once.  Stream: L0C chunks of L0T layer-0 tiles, then L1C
+//    chunks of L1T layer-1 row tiles, each followed by its two W2 operands.
+//  MODE 1 (H1 <= 256, Large): all T1 layer-1 accumulators live (T1 x 16 registers); layer-0 tiles
+//    are produced one at a time and consumed at once by every layer-1 tile.  Stream: chunks of L0T
+//    units {W0 tile t [KQ0], W1 k-steps of t for every row tile [T1][2]}, then W2 [T1][2].
+template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_>
 struct Net {
   // inputs padded to whole k-steps, with two spare columns IN, IN+1 = 1.0 carrying b0 as a
   // bf16 hi + lo pair, so layer 0's bias is added inside the MFMA at ~f32 precision
-  static constexpr int IN = IN_, INP = (IN_ + 2 + 15) / 16 * 16, H0 = H0_, H1 = H1_, CH = CH_;
+  static constexpr int IN = IN_, INP = (IN_ + 2 + 15) / 16 * 16, H0 = H0_, H1 = H1_, OUT = 9;
   static constexpr int KQ0 = INP / 16;        // layer-0 k-steps
   static constexpr int T0 = H0 / 32, T1 = H1 / 32;
-  static constexpr int NC = T0 / CH;          // chunks of layer-0 tiles per pass
-  // Layer-1 rows are produced in PASSES passes of T1P tiles (layer 0 is recomputed per pass), so
-  // the live accumulators are T1P x 16 registers: at H1 = 512 one pass would need all 256 AGPRs
-  // and the rest of the loop would spill.
-  static constexpr int PASSES = PASSES_, T1P = T1 / PASSES_;
-  static constexpr int OUT = 9;
-  // packed blob, in MFMA A operands (64 lanes x 16 B = 1 KiB each):
-  //   PASSES x NC chunks of { W0 [CH][KQ0], W1 rows of the pass [T1P][CH][2] }  (one LDS stage each)
-  //   W2 [T1][2], then f32 biases b0[H0], b1[H1], b2[32]
-  static constexpr int CW0 = CH * KQ0, CW1 = T1P * CH * 2, COPS = CW0 + CW1;
-  static constexpr int NCH = PASSES * NC;     // chunks in all
-  static constexpr int64_t CHUNKS_OPS = (int64_t)NCH * COPS;
-  static constexpr int64_t W2_OPS = (int64_t)T1 * 2;
-  static constexpr int64_t BIAS_OFF = (CHUNKS_OPS + W2_OPS) * 1024;
+  static constexpr int WAVES = WAVES_, MT = 64 * WAVES_, ROWS = 32 * WAVES_;   // samples per task
+  static constexpr int MODE = MODE_, L0T = L0T_, L1T = L1T_;
+  // operands (1 KiB MFMA A fragments) per unit and chunk
+  static constexpr int U0 = MODE == 0 ? KQ0 : KQ0 + 2 * T1;   // per layer-0 tile
+  static constexpr int U1 = 2 * T0 + 2;                       // MODE 0: per layer-1 row tile (+ its W2)
+  static constexpr int L0C = T0 / L0T, L0OPS = L0T * U0;
+  static constexpr int L1C = MODE == 0 ? T1 / L1T : 1, L1OPS = MODE == 0 ? L1T * U1 : 2 * T1;
+  static constexpr int NCH = L0C + L1C;
+  static constexpr int SOPS = L0OPS > L1OPS ? L0OPS : L1OPS;   // one LDS stage
+  static constexpr int64_t STREAM_OPS = (int64_t)L0C * L0OPS + (int64_t)L1C * L1OPS;
+  static constexpr int64_t BIAS_OFF = STREAM_OPS * 1024;
   static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
   static constexpr int STAGES = 2;            // chunk g in use, chunk g+1 landing
-  static constexpr int LDS_BYTES = STAGES * COPS * 1024 + 4 * (H0 + H1);
-  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % CH == 0 && T1 % PASSES == 0, "tile shapes");
-  static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + biases must fit the 160 KiB LDS");
+  static constexpr int LDS_BYTES = STAGES * SOPS * 1024 + 4 * H1;
+  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && T0 % L0T == 0 && (MODE == 1 || T1 % L1T == 0), "tile shapes");
+  static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + b1 must fit the 160 KiB LDS");
+  __host__ __device__ static constexpr int64_t chunk_off(int c) {
+    return c < L0C ? (int64_t)c * L0OPS : (int64_t)L0C * L0OPS + (int64_t)(c - L0C) * L1OPS;
+  }
+  __host__ __device__ static constexpr int chunk_ops(int c) { return c < L0C ? L0OPS : L1OPS; }
 };
 
 struct MlpArgs {
@@ -131,60 +142,35 @@ __device__ __forceinline__ void relu_to_frags_nb(f32x16 t, bf16x8& f0, bf16x8& f
   f1 = relu_bf16(__builtin_convertvector(hi, bf16x8));
 }
 
-// One chunk of packed weights (COPS operands) global -> LDS stage by LDS-DMA: each wave copies
-// every (MT/64)-th operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
+// Chunk c of the packed stream, global -> LDS stage by LDS-DMA: wave w copies every WAVES-th
+// operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
 template <class N>
-__device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4* dst, int w, int lane) {
-#pragma unroll
-  for (int o = w; o < N::COPS; o += MT / 64)
+__device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4* dst, int nops, int w, int lane) {
+  for (int o = w; o < nops; o += N::WAVES)
     __builtin_amdgcn_global_load_lds(src + o * 64 + lane, dst + o * 64, 16, 0, 0);
 }
 
-// Layer-0 MFMAs of one chunk: t0[m] = W0 tile (c*CH + m) . X^T  (accumulators only, no ReLU yet).
-// All CH*KQ0 A fragments are read first (one LDS round trip for the chunk, not one per MFMA).
-template <class N>
-__device__ __forceinline__ void layer0(const u32x4* S, const bf16x8 (&xb)[N::KQ0], int lane, f32x16 (&t0)[N::CH]) {
-  bf16x8 a[N::CH][N::KQ0];
-#pragma unroll
-  for (int m = 0; m < N::CH; ++m)
-#pragma unroll
-    for (int q = 0; q < N::KQ0; ++q) a[m][q] = frag(S + (m * N::KQ0 + q) * 64 + lane);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int m = 0; m < N::CH; ++m) {
-    t0[m] = f32x16{};
-#pragma unroll
-    for (int q = 0; q < N::KQ0; ++q) t0[m] = mfma(a[m][q], xb[q], t0[m]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// Layer-1 MFMAs of one chunk: MFMA i uses A operand CW0 + i (i = (n*CH + m)*2 + s) and
-// B = hb[m][s].  A fragments are read from LDS DEPTH groups of GS ahead of their MFMAs; the
-// sched_barriers keep the reads ahead of the MFMAs and stop the compiler from hoisting all CW1
-// reads at once (CW1 x 4 VGPRs would spill).
-template <class N>
-__device__ __forceinline__ void layer1(const u32x4* S, const bf16x8 (&hb)[N::CH][2], int lane,
-                                       f32x16 (&t1)[N::T1P]) {
-  constexpr int GS = 4, NG = N::CW1 / GS, DEPTH = 2;   // fragments read DEPTH groups ahead
-  static_assert(N::CW1 % GS == 0 && NG >= DEPTH, "layer-1 operand groups");
+// NOPS consecutive staged operands, each fed to MFMA f(i, A fragment): fragments are read from LDS
+// DEPTH groups of GS ahead of their MFMAs; the sched_barriers keep the reads ahead of the MFMAs and
+// stop the compiler from hoisting a whole chunk's reads (NOPS x 4 VGPRs would spill).
+template <int NOPS, class F>
+__device__ __forceinline__ void stream_ops(const u32x4* S, int lane, F&& f) {
+  constexpr int GS = NOPS % 4 == 0 ? 4 : 2, NG = NOPS / GS, DEPTH = 2;
+  static_assert(NOPS % GS == 0 && NG >= DEPTH, "operand groups");
   bf16x8 buf[DEPTH + 1][GS];
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
-    for (int i = 0; i < GS; ++i) buf[d][i] = frag(S + (N::CW0 + d * GS + i) * 64 + lane);
+    for (int i = 0; i < GS; ++i) buf[d][i] = frag(S + (d * GS + i) * 64 + lane);
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) {
     if (gi + DEPTH < NG) {
 #pragma unroll
-      for (int i = 0; i < GS; ++i) buf[(gi + DEPTH) % (DEPTH + 1)][i] = frag(S + (N::CW0 + (gi + DEPTH) * GS + i) * 64 + lane);
+      for (int i = 0; i < GS; ++i) buf[(gi + DEPTH) % (DEPTH + 1)][i] = frag(S + ((gi + DEPTH) * GS + i) * 64 + lane);
     }
     __builtin_amdgcn_sched_barrier(0);             // later groups' reads issue BEFORE this group's MFMAs
 #pragma unroll
-    for (int i = 0; i < GS; ++i) {
-      const int op = gi * GS + i, s = op & 1, m = (op >> 1) % N::CH, n = (op >> 1) / N::CH;
-      t1[n] = mfma(buf[gi % (DEPTH + 1)][i], hb[m][s], t1[n]);
-    }
+    for (int i = 0; i < GS; ++i) f(gi * GS + i, buf[gi % (DEPTH + 1)][i]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -242,32 +228,32 @@ __device__ __forceinline__ void emit_logits(const f32x16& lg, const float* b2, i
 }
 
 template <class N>
-__global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
-  // two weight stages + both hidden biases; A fragments are ds_read_b128 at operand*1 KiB +
-  // lane*16: conflict-free, and each 1 KiB operand is read by all 8 waves.
+__global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
+  // two weight stages + b1; A fragments are ds_read_b128 at operand*1 KiB + lane*16: conflict-free,
+  // and each 1 KiB operand is read by all WAVES waves.
   // ONE __shared__ object: with a second one beside the LDS-DMA target, hipcc (ROCm 7.2) emits
   // vmcnt(0) before ds_reads and the staging stops overlapping (cdna_hip_programming.md §5, trap (a))
-  __shared__ __attribute__((aligned(16))) u32x4 lds[N::STAGES * N::COPS * 64 + (N::H0 + N::H1) / 4];
-  u32x4 (*stage)[N::COPS * 64] = reinterpret_cast<u32x4 (*)[N::COPS * 64]>(lds);
-  float* bias = reinterpret_cast<float*>(lds + N::STAGES * N::COPS * 64);
+  __shared__ __attribute__((aligned(16))) u32x4 lds[N::STAGES * N::SOPS * 64 + N::H1 / 4];
+  float* b1s = reinterpret_cast<float*>(lds + N::STAGES * N::SOPS * 64);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (LDS-DMA base in m0)
   const int r = lane & 31, h = lane >> 5;
   const u32x4* chunks = static_cast<const u32x4*>(a.packed);
-  const u32x4* W2 = chunks + N::CHUNKS_OPS * 64;
   const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
   const float* b2 = gb + N::H0 + N::H1;
-  // Persistent: one workgroup per CU walks the 256-row tasks, so the weight pipeline (and the
-  // biases) carry over from task to task instead of restarting behind every workgroup's prologue.
-  const int64_t ntask = (a.rows + MT / 2 - 1) / (MT / 2);
+  // Persistent: one workgroup per CU walks the ROWS-sample tasks, so the weight pipeline (and b1)
+  // carry over from task to task instead of restarting behind every workgroup's prologue.
+  const int64_t ntask = (a.rows + N::ROWS - 1) / N::ROWS;
   const int my_tasks = (int)((ntask - blockIdx.x + gridDim.x - 1) / gridDim.x);
 
-  for (int i = tid; i < N::H0 + N::H1; i += MT) bias[i] = gb[i];
-  auto stage_of = [&](int gg) { return stage[gg % N::STAGES]; };
-  // running chunk counter gg = task_iter * NCH + g; chunk gg is weight chunk gg % NCH
+  for (int i = tid; i < N::H1; i += N::MT) b1s[i] = gb[N::H0 + i];
+  auto stage_of = [&](int gg) { return lds + (gg & 1) * (N::SOPS * 64); };
+  // running chunk counter gg = task_iter * NCH + c; chunk gg is stream chunk gg % NCH
   auto fetch = [&](int gg) {
-    if (gg < my_tasks * N::NCH && !(a.ablate & 1))
-      stage_chunk<N>(chunks + (int64_t)(gg % N::NCH) * N::COPS * 64, stage_of(gg), w, lane);
+    if (gg < my_tasks * N::NCH && !(a.ablate & 1)) {
+      const int c = gg % N::NCH;
+      stage_chunk<N>(chunks + N::chunk_off(c) * 64, stage_of(gg), N::chunk_ops(c), w, lane);
+    }
   };
   fetch(0);
   __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): chunk 0 landed
@@ -275,8 +261,7 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
 
   for (int it = 0; it < my_tasks; ++it) {
     const int64_t task = blockIdx.x + (int64_t)it * gridDim.x;
-    const int64_t s0 = task * (MT / 2) + w * 32;
-    const int64_t row = s0 + r;
+    const int64_t row = task * N::ROWS + w * 32 + r;
     const bool live = row < a.rows;               // (a wave past the end still joins the barriers)
     const int base = it * N::NCH;
     bf16x8 xb[N::KQ0];                            // X^T fragments: lane (r,h) holds obs[row][16q+8h+j]
@@ -295,35 +280,75 @@ __global__ __launch_bounds__(MT) void k_mlp(MlpArgs a) {
       }
     }
 
-    // Per chunk: layer 0 (bias inside the MFMA) -> ReLU -> layer 1, while chunk g+1 lands.  The
-    // ReLU's dependency bubble in one wave is covered by the other wave on the same SIMD.
     f32x16 lg{};
-    for (int p = 0; p < N::PASSES; ++p) {
-      const int g0 = base + p * N::NC;
-      f32x16 t1[N::T1P];
+    if constexpr (N::MODE == 0) {
+      // layer 0, once: every hidden unit of the wave's 32 samples as bf16 fragments in registers
+      bf16x8 hb[N::T0][2];
 #pragma unroll
-      for (int n = 0; n < N::T1P; ++n) t1[n] = f32x16{};
-      for (int c = 0; c < N::NC; ++c) {
-        const int g = g0 + c;
+      for (int c = 0; c < N::L0C; ++c) {
+        const int g = base + c;
         fetch(g + 1);
-        f32x16 t0[N::CH];
-        layer0<N>(stage_of(g), xb, lane, t0);
-        bf16x8 hb[N::CH][2];
-#pragma unroll
-        for (int m = 0; m < N::CH; ++m) relu_to_frags_nb(t0[m], hb[m][0], hb[m][1]);
-        layer1<N>(stage_of(g), hb, lane, t1);
+        f32x16 acc{};
+        stream_ops<N::L0OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
+          const int m = i / N::KQ0, q = i % N::KQ0;
+          acc = mfma(af, xb[q], q == 0 ? f32x16{} : acc);
+          if (q == N::KQ0 - 1) relu_to_frags_nb(acc, hb[c * N::L0T + m][0], hb[c * N::L0T + m][1]);
+        });
         __builtin_amdgcn_s_waitcnt(0x0F70);       // chunk g+1 landed
         __syncthreads();                          // ... and stage g is free for chunk g+2
       }
-      // layer 2 over this pass's hidden tiles
-#pragma unroll
-      for (int nn = 0; nn < N::T1P; ++nn) {
-        const int n = p * N::T1P + nn;
+      // layer 1 row tile by row tile (K = H0 from the registers), each tile's bias + ReLU feeding
+      // its two layer-2 MFMAs at once
+      for (int d = 0; d < N::L1C; ++d) {
+        const int g = base + N::L0C + d;
+        fetch(g + 1);
+        f32x16 acc{};
         bf16x8 f0, f1;
-        relu_to_frags(t1[nn], bias + N::H0, 32 * n, h, f0, f1);
-        lg = mfma(frag(W2 + ((int64_t)n * 2 + 0) * 64 + lane), f0, lg);
-        lg = mfma(frag(W2 + ((int64_t)n * 2 + 1) * 64 + lane), f1, lg);
-        __builtin_amdgcn_sched_barrier(0);        // one tile at a time: no hoisting of all tiles
+        stream_ops<N::L1OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
+          const int nn = i / N::U1, k = i % N::U1;
+          if (k < 2 * N::T0) {
+            acc = mfma(af, hb[k >> 1][k & 1], k == 0 ? f32x16{} : acc);
+            if (k == 2 * N::T0 - 1) relu_to_frags(acc, b1s, 32 * (d * N::L1T + nn), h, f0, f1);
+          } else {
+            lg = mfma(af, k == 2 * N::T0 ? f0 : f1, lg);
+          }
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+    } else {
+      // every layer-1 accumulator live; layer-0 tiles streamed through them
+      f32x16 acc1[N::T1];
+#pragma unroll
+      for (int n = 0; n < N::T1; ++n) acc1[n] = f32x16{};
+      for (int c = 0; c < N::L0C; ++c) {
+        const int g = base + c;
+        fetch(g + 1);
+        f32x16 acc0{};
+        bf16x8 hb0, hb1;
+        stream_ops<N::L0OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
+          const int k = i % N::U0;
+          if (k < N::KQ0) {
+            acc0 = mfma(af, xb[k], k == 0 ? f32x16{} : acc0);
+            if (k == N::KQ0 - 1) relu_to_frags_nb(acc0, hb0, hb1);
+          } else {
+            const int j = k - N::KQ0;
+            acc1[j >> 1] = mfma(af, (j & 1) ? hb1 : hb0, acc1[j >> 1]);
+          }
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+      {
+        const int g = base + N::L0C;
+        fetch(g + 1);
+        bf16x8 f0, f1;
+        stream_ops<N::L1OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
+          if ((i & 1) == 0) relu_to_frags(acc1[i >> 1], b1s, 32 * (i >> 1), h, f0, f1);
+          lg = mfma(af, (i & 1) ? f1 : f0, lg);
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
       }
     }
 
@@ -456,34 +481,46 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
   auto put = [&](int64_t op, int lane, int j, float v) { f[(op * 64 + lane) * 8 + j] = to_bf16(v); };
   // k order of an accumulator-as-operand fragment (layers 1, 2)
   auto kperm = [](int i, int s, int l, int j) { return 32 * i + 16 * s + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3); };
-  for (int g = 0; g < N::NCH; ++g) {
-    const int p = g / N::NC, c = g % N::NC;
-    const int64_t base = (int64_t)g * N::COPS;
-    for (int m = 0; m < N::CH; ++m) {
-      const int t = c * N::CH + m;               // layer-0 row tile
-      for (int q = 0; q < N::KQ0; ++q)           // W0 [H0][IN], natural k order (X^T from memory)
+  auto w1op = [&](int64_t op, int n, int t, int s) {   // W1 [H1][H0]: row tile n, k-step (t, s)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) put(op, l, j, w1[(int64_t)(32 * n + (l & 31)) * N::H0 + kperm(t, s, l, j)]);
+  };
+  auto w2op = [&](int64_t op, int n, int s) {          // W2 [9][H1]: k-step (n, s), rows padded to 32
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int o = l & 31;
+        put(op, l, j, o < N::OUT ? w2[(int64_t)o * N::H1 + kperm(n, s, l, j)] : 0.0f);
+      }
+  };
+  for (int c = 0; c < N::L0C; ++c)
+    for (int m = 0; m < N::L0T; ++m) {
+      const int t = c * N::L0T + m;                // layer-0 row tile
+      const int64_t base = N::chunk_off(c) + (int64_t)m * N::U0;
+      for (int q = 0; q < N::KQ0; ++q)             // W0 [H0][IN], natural k order (X^T from memory)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 8; ++j) {
             const int k = 16 * q + 8 * (l >> 5) + j, o = 32 * t + (l & 31);
             const float bh = from_bf16(to_bf16(b0[o]));        // b0 = hi + lo, both bf16
             const float v = k < N::IN ? w0[(int64_t)o * N::IN + k] : k == N::IN ? bh : k == N::IN + 1 ? b0[o] - bh : 0.0f;
-            put(base + m * N::KQ0 + q, l, j, v);
+            put(base + q, l, j, v);
           }
-      for (int nn = 0; nn < N::T1P; ++nn)        // W1 [H1][H0], rows of pass p
-        for (int s = 0; s < 2; ++s)
-          for (int l = 0; l < 64; ++l)
-            for (int j = 0; j < 8; ++j)
-              put(base + N::CW0 + (nn * N::CH + m) * 2 + s, l, j,
-                  w1[(int64_t)(32 * (p * N::T1P + nn) + (l & 31)) * N::H0 + kperm(t, s, l, j)]);
+      if (N::MODE == 1)                             // this tile's k-steps of every layer-1 row tile
+        for (int n = 0; n < N::T1; ++n)
+          for (int s = 0; s < 2; ++s) w1op(base + N::KQ0 + 2 * n + s, n, t, s);
     }
+  if (N::MODE == 0) {
+    for (int d = 0; d < N::L1C; ++d)
+      for (int nn = 0; nn < N::L1T; ++nn) {
+        const int n = d * N::L1T + nn;             // layer-1 row tile
+        const int64_t base = N::chunk_off(N::L0C + d) + (int64_t)nn * N::U1;
+        for (int t = 0; t < N::T0; ++t)
+          for (int s = 0; s < 2; ++s) w1op(base + 2 * t + s, n, t, s);
+        for (int s = 0; s < 2; ++s) w2op(base + 2 * N::T0 + s, n, s);
+      }
+  } else {
+    for (int n = 0; n < N::T1; ++n)
+      for (int s = 0; s < 2; ++s) w2op(N::chunk_off(N::L0C) + 2 * n + s, n, s);
   }
-  for (int i = 0; i < N::T1; ++i)                // W2 [9][H1], rows padded to 32 with zeros
-    for (int s = 0; s < 2; ++s)
-      for (int l = 0; l < 64; ++l)
-        for (int j = 0; j < 8; ++j) {
-          const int o = l & 31;
-          put(N::CHUNKS_OPS + i * 2 + s, l, j, o < N::OUT ? w2[(int64_t)o * N::H1 + kperm(i, s, l, j)] : 0.0f);
-        }
   float* bias = reinterpret_cast<float*>(blob.data() + N::BIAS_OFF);
   memcpy(bias, b0, 4 * N::H0);
   memcpy(bias + N::H0, b1, 4 * N::H1);
@@ -528,29 +565,32 @@ std::vector<uint8_t> pack_f32(const float* w0, const float* b0, const float* w1,
 
 struct MlpKernel {
   int in, h0, h1, precision;
+  int threads, rows_per_task;
   int64_t bytes;
   void (*fwd)(MlpArgs);
   std::vector<uint8_t> (*pack)(const float*, const float*, const float*, const float*, const float*, const float*);
 };
 
-template <int IN, int H0, int H1, int CH, int PASSES>
+template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T>
 MlpKernel make_mlp() {
-  using N = Net<IN, H0, H1, CH, PASSES>;
-  return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::BYTES, k_mlp<N>, pack<N>};
+  using N = Net<IN, H0, H1, WAVES, MODE, L0T, L1T>;
+  return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp<N>, pack<N>};
 }
 
 template <int IN, int H0, int H1, int PASSES>
 MlpKernel make_mlp_f32() {
   using N = NetF<IN, H0, H1, PASSES>;
-  return MlpKernel{IN, H0, H1, WH_MLP_F32, N::BYTES, k_mlp_f32<N>, pack_f32<N>};
+  return MlpKernel{IN, H0, H1, WH_MLP_F32, 256, 128, N::BYTES, k_mlp_f32<N>, pack_f32<N>};
 }
 
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml
   static const MlpKernel reg[] = {
-      make_mlp<37, 256, 256, 4, 2>(),     // Small:  obs 9*4+1,  [256, 256]
-      make_mlp<82, 512, 512, 4, 4>(),     // Medium: obs 9*9+1,  [512, 512]
-      make_mlp<145, 1024, 256, 2, 2>(),   // Large:  obs 9*16+1, [1024, 256]
+      // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk):
+      // 8 waves = two per SIMD (256 registers each)
+      make_mlp<37, 256, 256, 8, 0, 8, 4>(),     // Small:  obs 9*4+1,  [256, 256]
+      make_mlp<82, 512, 512, 8, 0, 8, 2>(),     // Medium: obs 9*9+1,  [512, 512]
+      make_mlp<145, 1024, 256, 8, 1, 2, 1>(),   // Large:  obs 9*16+1, [1024, 256]
       make_mlp_f32<37, 256, 256, 1>(),    // the same shapes in exact f32
       make_mlp_f32<82, 512, 512, 2>(),
       make_mlp_f32<145, 1024, 256, 1>(),
@@ -606,9 +646,9 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
     hipLaunchKernelGGL(k->fwd, dim3((unsigned)((ntask + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
     return hip_rc(hipGetLastError());
   }
-  const int64_t ntask = (rows + MT / 2 - 1) / (MT / 2);
+  const int64_t ntask = (rows + k->rows_per_task - 1) / k->rows_per_task;
   const unsigned grid = (unsigned)(ntask < cus ? ntask : cus);
-  hipLaunchKernelGGL(k->fwd, dim3(grid), dim3(MT), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k->fwd, dim3(grid), dim3(k->threads), 0, (hipStream_t)stream, a);
   return hip_rc(hipGetLastError());
 }
 
