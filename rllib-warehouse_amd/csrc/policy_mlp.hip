@@ -13,13 +13,12 @@
 //    ReLU + v_cvt_pk_bf16_f32, registers 8s..8s+7 ARE the B operand of k-step s of the next layer
 //    (cdna_hip_programming.md §3, "accumulator tile as the next MFMA's operand"): activations
 //    never leave registers.  The permuted k order this implies is folded into the packed weights.
-//  * Layer 0 is streamed in chunks of CH hidden tiles straight into layer 1's accumulators, and
-//    layer-1 rows are produced in PASSES passes, so only T1P x 16 accumulator registers (+ one
-//    chunk) are live: <= 256 registers per lane, two waves per SIMD (8 per workgroup).
+//  * Every layer runs once per sample (struct Net: MODE 0 keeps all layer-0 activations, MODE 1
+//    all layer-1 accumulators, whichever fits 256 registers at two waves per SIMD).
 //  * Layer 0's bias rides in the MFMA (two input columns fixed at 1.0 carry b0 as bf16 hi + lo);
 //    ReLU runs on the packed bf16 bits (v_pk_max_i16 with 0).
-//  * Weights are packed once (wh_mlp_pack) in fragment order, one MFMA A operand = 64 lanes x 16
-//    contiguous bytes, and streamed chunk by chunk into two LDS stages by LDS-DMA
+//  * Weights are packed once (wh_mlp_pack) in consumption order, one MFMA A operand = 64 lanes x
+//    16 contiguous bytes, and streamed chunk by chunk into two LDS stages by LDS-DMA
 //    (global_load_lds_dwordx4, lane-linear); all 8 waves read every staged operand.
 //  * Persistent workgroups (one per CU) walk 256-row tasks, so the weight pipeline and the
 //    biases carry over from task to task.
@@ -54,7 +53,7 @@ constexpr uint32_t PUR_MLP = 5;         // philox purpose (1-4 are the simulator
 //  MODE 1 (H1 <= 256, Large): all T1 layer-1 accumulators live (T1 x 16 registers); layer-0 tiles
 //    are produced one at a time and consumed at once by every layer-1 tile.  Stream: chunks of L0T
 //    units {W0 tile t [KQ0], W1 k-steps of t for every row tile [T1][2]}, then W2 [T1][2].
-template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_>
+template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_, bool XPF_ = false>
 struct Net {
   // inputs padded to whole k-steps, with two spare columns IN, IN+1 = 1.0 carrying b0 as a
   // bf16 hi + lo pair, so layer 0's bias is added inside the MFMA at ~f32 precision
@@ -63,6 +62,9 @@ struct Net {
   static constexpr int T0 = H0 / 32, T1 = H1 / 32;
   static constexpr int WAVES = WAVES_, MT = 64 * WAVES_, ROWS = 32 * WAVES_;   // samples per task
   static constexpr int MODE = MODE_, L0T = L0T_, L1T = L1T_;
+  // MODE 0: load the next task's X during layer 1 (registers permitting: measured a gain where
+  // T0 x 8 leaves room -- Small -- and a loss at Medium, whose 256 registers then spill)
+  static constexpr bool XPF = XPF_ && MODE == 0;
   // operands (1 KiB MFMA A fragments) per unit and chunk
   static constexpr int U0 = MODE == 0 ? KQ0 : KQ0 + 2 * T1;   // per layer-0 tile
   static constexpr int U1 = 2 * T0 + 2;                       // MODE 0: per layer-1 row tile (+ its W2)
@@ -142,6 +144,19 @@ __device__ __forceinline__ void relu_to_frags_nb(f32x16 t, bf16x8& f0, bf16x8& f
   f1 = relu_bf16(__builtin_convertvector(hi, bf16x8));
 }
 
+// Timing-only ablations (builds with -DWH_MLP_ABLATION, env WH_MLP_ABLATE; results are wrong):
+// 2 = no bias/ReLU/bf16 conversion (accumulator bits reused as fragments), 4 = no chunk barriers,
+// 8 = no observation loads.
+#ifdef WH_MLP_ABLATION
+#define MLP_ABL(a, bit) (((a).ablate & (bit)) != 0)
+#else
+#define MLP_ABL(a, bit) false
+#endif
+__device__ __forceinline__ void raw_frags(const f32x16& t, bf16x8& f0, bf16x8& f1) {
+  f0 = __builtin_bit_cast(bf16x8, (f32x4){t[0], t[1], t[2], t[3]});
+  f1 = __builtin_bit_cast(bf16x8, (f32x4){t[8], t[9], t[10], t[11]});
+}
+
 // Chunk c of the packed stream, global -> LDS stage by LDS-DMA: wave w copies every WAVES-th
 // operand, one global_load_lds_dwordx4 (1 KiB, lane-linear) per operand.
 template <class N>
@@ -153,9 +168,9 @@ __device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4
 // NOPS consecutive staged operands, each fed to MFMA f(i, A fragment): fragments are read from LDS
 // DEPTH groups of GS ahead of their MFMAs; the sched_barriers keep the reads ahead of the MFMAs and
 // stop the compiler from hoisting a whole chunk's reads (NOPS x 4 VGPRs would spill).
-template <int NOPS, class F>
+template <int NOPS, int GS_ = 4, int DEPTH = 2, class F>
 __device__ __forceinline__ void stream_ops(const u32x4* S, int lane, F&& f) {
-  constexpr int GS = NOPS % 4 == 0 ? 4 : 2, NG = NOPS / GS, DEPTH = 2;
+  constexpr int GS = NOPS % GS_ == 0 ? GS_ : 2, NG = NOPS / GS;
   static_assert(NOPS % GS == 0 && NG >= DEPTH, "operand groups");
   bf16x8 buf[DEPTH + 1][GS];
 #pragma unroll
@@ -259,26 +274,57 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): chunk 0 landed
   __syncthreads();
 
+  // X^T fragments: lane (r,h) holds obs[row][16q+8h+j] (bias columns IN, IN+1 = 1.0)
+  // (raw values of k-steps [q0, q1) at xr[(q - q0) * 8 + j])
+  auto load_x = [&](int64_t xrow, float* xr, int q0 = 0, int q1 = N::KQ0) {
+    const float* x = a.obs + (xrow < a.rows ? xrow : 0) * N::IN;
+#pragma unroll
+    for (int q = q0; q < q1; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * q + 8 * h + j;
+        xr[(q - q0) * 8 + j] = MLP_ABL(a, 8) ? 0.5f : x[k < N::IN ? k : N::IN - 1];   // clamp, then select
+      }
+  };
+  auto cvt_x = [&](const float* xr, bool lv, bf16x8 (&xb)[N::KQ0], int q0 = 0, int q1 = N::KQ0) {
+#pragma unroll
+    for (int q = q0; q < q1; ++q) {
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * q + 8 * h + j;
+        v[j] = k < N::IN ? (lv ? xr[(q - q0) * 8 + j] : 0.0f) : (k < N::IN + 2 ? 1.0f : 0.0f);
+      }
+      xb[q] = __builtin_convertvector(v, bf16x8);
+    }
+  };
+  bf16x8 xb[N::KQ0];
+  if (my_tasks > 0) {
+    const int64_t row0 = (int64_t)blockIdx.x * N::ROWS + w * 32 + r;
+    float xr[N::KQ0 * 8];
+    load_x(row0, xr);
+    cvt_x(xr, row0 < a.rows, xb);
+  }
+
   for (int it = 0; it < my_tasks; ++it) {
     const int64_t task = blockIdx.x + (int64_t)it * gridDim.x;
     const int64_t row = task * N::ROWS + w * 32 + r;
     const bool live = row < a.rows;               // (a wave past the end still joins the barriers)
     const int base = it * N::NCH;
-    bf16x8 xb[N::KQ0];                            // X^T fragments: lane (r,h) holds obs[row][16q+8h+j]
-    {
-      const float* x = a.obs + (live ? row : 0) * N::IN;
-#pragma unroll
-      for (int q = 0; q < N::KQ0; ++q) {
-        f32x8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 16 * q + 8 * h + j;
-          const float xv = x[k < N::IN ? k : N::IN - 1];      // branch-free: clamp, then select
-          v[j] = k < N::IN ? (live ? xv : 0.0f) : (k < N::IN + 2 ? 1.0f : 0.0f);   // bias columns
-        }
-        xb[q] = __builtin_convertvector(v, bf16x8);
-      }
+    if (!N::XPF && it > 0) {                      // X of this task, loaded now
+      float xr[N::KQ0 * 8];
+      load_x(row, xr);
+      cvt_x(xr, live, xb);
     }
+    // MODE 0: the NEXT task's rows are loaded during layer-1 chunks and converted after their
+    // barriers (X is dead once layer 0 is done), so no task starts behind an HBM round trip; in NS
+    // parts of QP k-steps, part p during chunk PF + p, to keep the raw f32 values within the
+    // register budget
+    constexpr int NS = N::L1C >= 3 ? 2 : 1;      // parts, one per chunk
+    constexpr int QP = (N::KQ0 + NS - 1) / NS, PF = N::L1C - 1 - NS;  // k-steps per part, first chunk
+    static_assert(N::MODE == 1 || PF >= 0, "layer-1 chunks to prefetch in");
+    const int64_t row_next = row + (int64_t)gridDim.x * N::ROWS;
+    const bool has_next = it + 1 < my_tasks;
 
     f32x16 lg{};
     if constexpr (N::MODE == 0) {
@@ -292,29 +338,45 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
         stream_ops<N::L0OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
           const int m = i / N::KQ0, q = i % N::KQ0;
           acc = mfma(af, xb[q], q == 0 ? f32x16{} : acc);
-          if (q == N::KQ0 - 1) relu_to_frags_nb(acc, hb[c * N::L0T + m][0], hb[c * N::L0T + m][1]);
+          if (q == N::KQ0 - 1) {
+            if (MLP_ABL(a, 2)) raw_frags(acc, hb[c * N::L0T + m][0], hb[c * N::L0T + m][1]);
+            else relu_to_frags_nb(acc, hb[c * N::L0T + m][0], hb[c * N::L0T + m][1]);
+          }
         });
-        __builtin_amdgcn_s_waitcnt(0x0F70);       // chunk g+1 landed
-        __syncthreads();                          // ... and stage g is free for chunk g+2
+        if (!MLP_ABL(a, 4)) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);     // chunk g+1 landed
+          __syncthreads();                        // ... and stage g is free for chunk g+2
+        }
       }
       // layer 1 row tile by row tile (K = H0 from the registers), each tile's bias + ReLU feeding
       // its two layer-2 MFMAs at once
       for (int d = 0; d < N::L1C; ++d) {
         const int g = base + N::L0C + d;
         fetch(g + 1);
+        float xr[QP * 8];                         // one part at a time
+        if (N::XPF && d == PF && has_next) load_x(row_next, xr, 0, QP);
+        if (N::XPF && NS == 2 && d == PF + 1 && has_next) load_x(row_next, xr, QP, N::KQ0);
         f32x16 acc{};
         bf16x8 f0, f1;
-        stream_ops<N::L1OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
+        // with the X prefetch: 4-op groups one group ahead (fewer fragments in flight)
+        stream_ops<N::L1OPS, 4, N::XPF ? 1 : 2>(stage_of(g), lane, [&](int i, bf16x8 af) {
           const int nn = i / N::U1, k = i % N::U1;
           if (k < 2 * N::T0) {
             acc = mfma(af, hb[k >> 1][k & 1], k == 0 ? f32x16{} : acc);
-            if (k == 2 * N::T0 - 1) relu_to_frags(acc, b1s, 32 * (d * N::L1T + nn), h, f0, f1);
+            if (k == 2 * N::T0 - 1) {
+              if (MLP_ABL(a, 2)) raw_frags(acc, f0, f1);
+              else relu_to_frags(acc, b1s, 32 * (d * N::L1T + nn), h, f0, f1);
+            }
           } else {
             lg = mfma(af, k == 2 * N::T0 ? f0 : f1, lg);
           }
         });
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
+        if (!MLP_ABL(a, 4)) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          __syncthreads();
+        }
+        if (N::XPF && d == PF && has_next) cvt_x(xr, row_next < a.rows, xb, 0, QP);
+        if (N::XPF && NS == 2 && d == PF + 1 && has_next) cvt_x(xr, row_next < a.rows, xb, QP, N::KQ0);
       }
     } else {
       // every layer-1 accumulator live; layer-0 tiles streamed through them
@@ -330,25 +392,35 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
           const int k = i % N::U0;
           if (k < N::KQ0) {
             acc0 = mfma(af, xb[k], k == 0 ? f32x16{} : acc0);
-            if (k == N::KQ0 - 1) relu_to_frags_nb(acc0, hb0, hb1);
+            if (k == N::KQ0 - 1) {
+              if (MLP_ABL(a, 2)) raw_frags(acc0, hb0, hb1);
+              else relu_to_frags_nb(acc0, hb0, hb1);
+            }
           } else {
             const int j = k - N::KQ0;
             acc1[j >> 1] = mfma(af, (j & 1) ? hb1 : hb0, acc1[j >> 1]);
           }
         });
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
+        if (!MLP_ABL(a, 4)) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          __syncthreads();
+        }
       }
       {
         const int g = base + N::L0C;
         fetch(g + 1);
         bf16x8 f0, f1;
         stream_ops<N::L1OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
-          if ((i & 1) == 0) relu_to_frags(acc1[i >> 1], b1s, 32 * (i >> 1), h, f0, f1);
+          if ((i & 1) == 0) {
+            if (MLP_ABL(a, 2)) raw_frags(acc1[i >> 1], f0, f1);
+            else relu_to_frags(acc1[i >> 1], b1s, 32 * (i >> 1), h, f0, f1);
+          }
           lg = mfma(af, (i & 1) ? f1 : f0, lg);
         });
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
+        if (!MLP_ABL(a, 4)) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          __syncthreads();
+        }
       }
     }
 
@@ -571,9 +643,9 @@ struct MlpKernel {
   std::vector<uint8_t> (*pack)(const float*, const float*, const float*, const float*, const float*, const float*);
 };
 
-template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T>
+template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T, bool XPF>
 MlpKernel make_mlp() {
-  using N = Net<IN, H0, H1, WAVES, MODE, L0T, L1T>;
+  using N = Net<IN, H0, H1, WAVES, MODE, L0T, L1T, XPF>;
   return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp<N>, pack<N>};
 }
 
@@ -586,11 +658,11 @@ MlpKernel make_mlp_f32() {
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml
   static const MlpKernel reg[] = {
-      // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk):
-      // 8 waves = two per SIMD (256 registers each)
-      make_mlp<37, 256, 256, 8, 0, 8, 4>(),     // Small:  obs 9*4+1,  [256, 256]
-      make_mlp<82, 512, 512, 8, 0, 8, 2>(),     // Medium: obs 9*9+1,  [512, 512]
-      make_mlp<145, 1024, 256, 8, 1, 2, 1>(),   // Large:  obs 9*16+1, [1024, 256]
+      // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk,
+      // next-task X prefetch): 8 waves = two per SIMD (256 registers each)
+      make_mlp<37, 256, 256, 8, 0, 8, 4, true>(),     // Small:  obs 9*4+1,  [256, 256]
+      make_mlp<82, 512, 512, 8, 0, 8, 2, false>(),    // Medium: obs 9*9+1,  [512, 512]
+      make_mlp<145, 1024, 256, 8, 1, 2, 1, false>(),  // Large:  obs 9*16+1, [1024, 256]
       make_mlp_f32<37, 256, 256, 1>(),    // the same shapes in exact f32
       make_mlp_f32<82, 512, 512, 2>(),
       make_mlp_f32<145, 1024, 256, 1>(),

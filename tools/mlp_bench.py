@@ -9,8 +9,9 @@ import warehouse  # noqa: E402
 import warehouse.policy as wp  # noqa: E402
 
 B = int(os.environ.get("MLP_B", 65536))
+VARIANTS = os.environ.get("MLP_VARIANTS", "small,medium,large").split(",")
 for abl, variant, na in [(a, v, n) for a in os.environ.get("MLP_ABLATE", "0").split(",")
-                         for v, n in (("small", 4), ("medium", 8), ("large", 16))]:
+                         for v, n in (("small", 4), ("medium", 8), ("large", 16)) if v in VARIANTS]:
     os.environ["WH_MLP_ABLATE"] = abl
     net = wp.MLPPolicy(variant, seed=1)
     rows = B * na
