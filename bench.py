@@ -347,11 +347,23 @@ def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     B, NA = env.B, env.agent_slots
     acts = torch.empty((B, NA), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    obs = env.observe()
+    # bf16: the observation rows go to the network as its layer-0 operand (wh_observe_x, bf16 in
+    # MFMA fragment order; the same inputs as rounding the f32 rows) -- nothing else reads them on
+    # this route; f32: the float32 rows
+    frag = precision == "bf16"
+    obs = env.observe_x() if frag else env.observe()
+
+    def infer():
+        if frag:
+            net.forward_x(obs, B * NA, step=0, actions=acts.view(-1))
+        else:
+            net(obs.view(B * NA, -1), step=0, actions=acts.view(-1))
 
     def one():
-        net(obs.view(B * NA, -1), step=0, actions=acts.view(-1))
-        env.vector_step(acts, autoreset=True, observe=True)
+        infer()
+        env.vector_step(acts, autoreset=True, observe=not frag)
+        if frag:
+            env.observe_x()
 
     for _ in range(max(min(W, 20), 3)):
         one()
@@ -374,7 +386,7 @@ def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     for a, b in evs:
         a.record(stream)
         for _ in range(5):
-            net(obs.view(B * NA, -1), step=0, actions=acts.view(-1))
+            infer()
         b.record(stream)
     torch.cuda.synchronize(dev)
     kms = sorted(a.elapsed_time(b) / 5 for a, b in evs)
@@ -509,8 +521,10 @@ def main():
             peak = MFMA_BF16_PEAK_TFS if prec == "bf16" else MFMA_F32_PEAK_TFS
             line = {
                 "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
-                            f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset + "
-                            f"observation rows); random-init weights (no checkpoint ships with the reference)",
+                            f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> wh_vector_step (step + auto-reset) -> "
+                            + ("observation rows as the MLP's bf16 fragment-order operand (wh_observe_x)" if prec == "bf16"
+                               else "f32 observation rows") +
+                            "; random-init weights (no checkpoint ships with the reference)",
                 "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,
                 "ms_per_step": el4 * 1e3 / Kp,
                 "dtype": "bf16 MFMA, f32 accumulate" if prec == "bf16" else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",

@@ -124,6 +124,13 @@ int wh_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* act
  *   self_availability, self_delivery_target, self_position
  * obs [B,NA,9R+1] float32; rows of slots >= n are zero. */
 int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* stream);
+/* wh_observe plus (xfrag != NULL) the same rows as the SAC policy network's layer-0 operand, for
+ * wh_mlp_forward_x: bf16 in MFMA fragment order, ceil(B*NA/32) tiles of 32 agent rows x KQ =
+ * ceil((9R+3)/16) k-steps x 64 lanes x 16 bytes; 16-byte chunk ((tile*KQ + q)*64 + lane) = features
+ * 16q + 8(lane>>5) + j, j < 8, of row tile*32 + (lane&31), features 9R+1 and 9R+2 = 1.0, padding 0
+ * (rows past B*NA: zero features but the two 1.0 columns).  obs may be NULL.  WH_ENOTSUP for agent counts whose
+ * observation workgroups do not hold whole 32-row tiles (e.g. Medium with 9 agents). */
+int wh_observe_x(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* xfrag, void* stream);
 
 #define WH_POLICY_GREEDY 1    /* baseline/solvers.py:27-58 with random_action_prob p */
 #define WH_POLICY_RANDOM 2    /* uniform over the 9 moves (action_space.sample()) */
@@ -217,6 +224,12 @@ int wh_mlp_pack(const wh_mlp_desc* d, const float* w0, const float* b0, const fl
 int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const float* obs,
                    float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
                    void* stream);
+/* wh_mlp_forward with the observation rows given as wh_observe_x's fragment-order operand (bf16
+ * precision only; the same logits as wh_mlp_forward on the f32 rows, which it rounds to bf16
+ * exactly so): one coalesced 16-byte load per k-step and lane instead of strided f32 rows. */
+int wh_mlp_forward_x(const wh_mlp_desc* d, const void* packed, int64_t rows, const void* xfrag,
+                     float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
+                     void* stream);
 
 /* Library build identification (e.g. "warehouse_amd gfx950 <date>"). */
 const char* wh_version(void);

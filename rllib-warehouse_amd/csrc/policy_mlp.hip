@@ -94,6 +94,7 @@ struct MlpArgs {
   int32_t explore;
   uint32_t k0, k1, step;
   int32_t ablate;   // timing experiments only (env WH_MLP_ABLATE): 1 = no staging in the loop
+  const u32x4* xfrag;   // non-null: X already in fragment order (wh_observe_x), obs unused
 };
 
 __device__ __forceinline__ bf16x8 frag(const u32x4* p) { return __builtin_bit_cast(bf16x8, *p); }
@@ -146,7 +147,7 @@ __device__ __forceinline__ void relu_to_frags_nb(f32x16 t, bf16x8& f0, bf16x8& f
 
 // Timing-only ablations (builds with -DWH_MLP_ABLATION, env WH_MLP_ABLATE; results are wrong):
 // 2 = no bias/ReLU/bf16 conversion (accumulator bits reused as fragments), 4 = no chunk barriers,
-// 8 = no observation loads.
+// 8 = no observation loads, 16 = no wait for the next chunk's LDS-DMA before the barrier.
 #ifdef WH_MLP_ABLATION
 #define MLP_ABL(a, bit) (((a).ablate & (bit)) != 0)
 #else
@@ -298,12 +299,26 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
       xb[q] = __builtin_convertvector(v, bf16x8);
     }
   };
+  // fragment-order X (wh_observe_x): the wave's 32 rows are tile task * WAVES + w, one coalesced
+  // 16-byte load per k-step (tiles past the last row read tile 0: those rows are never emitted)
+  const bool xf = a.xfrag != nullptr;
+  auto load_xf = [&](int64_t task_i, bf16x8 (&xb)[N::KQ0]) {
+    int64_t tile = task_i * N::WAVES + w;
+    tile = tile * 32 < a.rows ? tile : 0;
+    const u32x4* src = a.xfrag + tile * (N::KQ0 * 64) + lane;
+#pragma unroll
+    for (int q = 0; q < N::KQ0; ++q) xb[q] = frag(src + q * 64);
+  };
   bf16x8 xb[N::KQ0];
   if (my_tasks > 0) {
-    const int64_t row0 = (int64_t)blockIdx.x * N::ROWS + w * 32 + r;
-    float xr[N::KQ0 * 8];
-    load_x(row0, xr);
-    cvt_x(xr, row0 < a.rows, xb);
+    if (xf) {
+      load_xf(blockIdx.x, xb);
+    } else {
+      const int64_t row0 = (int64_t)blockIdx.x * N::ROWS + w * 32 + r;
+      float xr[N::KQ0 * 8];
+      load_x(row0, xr);
+      cvt_x(xr, row0 < a.rows, xb);
+    }
   }
 
   for (int it = 0; it < my_tasks; ++it) {
@@ -311,7 +326,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
     const int64_t row = task * N::ROWS + w * 32 + r;
     const bool live = row < a.rows;               // (a wave past the end still joins the barriers)
     const int base = it * N::NCH;
-    if (!N::XPF && it > 0) {                      // X of this task, loaded now
+    if (!xf && !N::XPF && it > 0) {               // X of this task, loaded now
       float xr[N::KQ0 * 8];
       load_x(row, xr);
       cvt_x(xr, live, xb);
@@ -344,7 +359,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
           }
         });
         if (!MLP_ABL(a, 4)) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);     // chunk g+1 landed
+          if (!MLP_ABL(a, 16)) __builtin_amdgcn_s_waitcnt(0x0F70);     // chunk g+1 landed
           __syncthreads();                        // ... and stage g is free for chunk g+2
         }
       }
@@ -353,9 +368,11 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
       for (int d = 0; d < N::L1C; ++d) {
         const int g = base + N::L0C + d;
         fetch(g + 1);
+        // fragment-order X: the next task's operand straight into xb during the last chunk
+        if (xf && d == N::L1C - 1 && has_next) load_xf(task + gridDim.x, xb);
         float xr[QP * 8];                         // one part at a time
-        if (N::XPF && d == PF && has_next) load_x(row_next, xr, 0, QP);
-        if (N::XPF && NS == 2 && d == PF + 1 && has_next) load_x(row_next, xr, QP, N::KQ0);
+        if (!xf && N::XPF && d == PF && has_next) load_x(row_next, xr, 0, QP);
+        if (!xf && N::XPF && NS == 2 && d == PF + 1 && has_next) load_x(row_next, xr, QP, N::KQ0);
         f32x16 acc{};
         bf16x8 f0, f1;
         // with the X prefetch: 4-op groups one group ahead (fewer fragments in flight)
@@ -372,11 +389,11 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
           }
         });
         if (!MLP_ABL(a, 4)) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);
+          if (!MLP_ABL(a, 16)) __builtin_amdgcn_s_waitcnt(0x0F70);
           __syncthreads();
         }
-        if (N::XPF && d == PF && has_next) cvt_x(xr, row_next < a.rows, xb, 0, QP);
-        if (N::XPF && NS == 2 && d == PF + 1 && has_next) cvt_x(xr, row_next < a.rows, xb, QP, N::KQ0);
+        if (!xf && N::XPF && d == PF && has_next) cvt_x(xr, row_next < a.rows, xb, 0, QP);
+        if (!xf && N::XPF && NS == 2 && d == PF + 1 && has_next) cvt_x(xr, row_next < a.rows, xb, QP, N::KQ0);
       }
     } else {
       // every layer-1 accumulator live; layer-0 tiles streamed through them
@@ -402,13 +419,14 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
           }
         });
         if (!MLP_ABL(a, 4)) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);
+          if (!MLP_ABL(a, 16)) __builtin_amdgcn_s_waitcnt(0x0F70);
           __syncthreads();
         }
       }
       {
         const int g = base + N::L0C;
         fetch(g + 1);
+        if (xf && has_next) load_xf(task + gridDim.x, xb);   // X is dead once layer 0 is done
         bf16x8 f0, f1;
         stream_ops<N::L1OPS>(stage_of(g), lane, [&](int i, bf16x8 af) {
           if ((i & 1) == 0) {
@@ -418,7 +436,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
           lg = mfma(af, (i & 1) ? f1 : f0, lg);
         });
         if (!MLP_ABL(a, 4)) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);
+          if (!MLP_ABL(a, 16)) __builtin_amdgcn_s_waitcnt(0x0F70);
           __syncthreads();
         }
       }
@@ -695,17 +713,18 @@ int wh_mlp_pack(const wh_mlp_desc* d, const float* w0, const float* b0, const fl
   return hip_rc(hipMemcpy(packed, blob.data(), blob.size(), hipMemcpyHostToDevice));
 }
 
-int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const float* obs,
-                   float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
-                   void* stream) {
+static int mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const float* obs,
+                       const void* xfrag, float* logits, int32_t* actions, int32_t explore, uint64_t seed,
+                       uint32_t step, void* stream) {
   const MlpKernel* k = find_mlp(d);
   if (!k) return d ? WH_ENOTSUP : WH_EINVAL;
   if (rows < 0) return WH_EINVAL;
   if (rows == 0) return WH_OK;
-  if (!packed || !obs || (!logits && !actions)) return WH_EINVAL;
+  if (!packed || (!obs && !xfrag) || (!logits && !actions)) return WH_EINVAL;
+  if (xfrag && (k->precision != WH_MLP_BF16 || (uintptr_t)xfrag % 16 != 0)) return WH_ENOTSUP;
   const char* abl = getenv("WH_MLP_ABLATE");
   MlpArgs a{packed, rows, obs, logits, actions, explore ? 1 : 0, (uint32_t)(seed & 0xFFFFFFFFu),
-            (uint32_t)(seed >> 32), step, abl ? atoi(abl) : 0};
+            (uint32_t)(seed >> 32), step, abl ? atoi(abl) : 0, static_cast<const u32x4*>(xfrag)};
   static int cus = 0;                         // one persistent workgroup per CU
   if (!cus) {
     int dev = 0;
@@ -722,6 +741,19 @@ int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const
   const unsigned grid = (unsigned)(ntask < cus ? ntask : cus);
   hipLaunchKernelGGL(k->fwd, dim3(grid), dim3(k->threads), 0, (hipStream_t)stream, a);
   return hip_rc(hipGetLastError());
+}
+
+int wh_mlp_forward(const wh_mlp_desc* d, const void* packed, int64_t rows, const float* obs,
+                   float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
+                   void* stream) {
+  return mlp_forward(d, packed, rows, obs, nullptr, logits, actions, explore, seed, step, stream);
+}
+
+int wh_mlp_forward_x(const wh_mlp_desc* d, const void* packed, int64_t rows, const void* xfrag,
+                     float* logits, int32_t* actions, int32_t explore, uint64_t seed, uint32_t step,
+                     void* stream) {
+  if (!xfrag) return WH_EINVAL;
+  return mlp_forward(d, packed, rows, nullptr, xfrag, logits, actions, explore, seed, step, stream);
 }
 
 }  // extern "C"

@@ -1279,10 +1279,16 @@ struct ObsLds {
   uint32_t dst[C::DP];           // delivery cell, x | y << 16
 };
 
+// xfrag (optional): the same rows as the policy network's layer-0 B operand (policy_mlp.hip),
+// bf16, in MFMA fragment order: 16-byte chunk ((tile * KQ + q) * 64 + lane) of agent-row tile
+// `tile` (32 rows) holds features 16q + 8h + j (j < 8) of row tile*32 + (lane & 31), h = lane >> 5;
+// features L, L+1 are 1.0 (the MLP's bias columns), the rest of the padding 0.  One coalesced
+// 16-byte load per k-step for the MLP instead of scattered f32 rows (and half the bytes).
 template <class C, int OBS_EB>
 __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ state, int64_t B, int na,
                                                 const uint32_t* __restrict__ tables,
-                                                float* __restrict__ obs, int quads) {
+                                                float* __restrict__ obs, int quads,
+                                                uint4* __restrict__ xfrag) {
   __shared__ ObsLds<C, OBS_EB> O;
   constexpr int OBS_PARTS = BT / OBS_EB;
   constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C, OBS_EB>::SRCW;
@@ -1350,6 +1356,38 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   }
   __syncthreads();
   const uint32_t per_env = (uint32_t)na * L;
+  if (xfrag) {
+    // the group's rows are whole 32-row tiles (OBS_EB * na % 32 == 0, checked on the host)
+    constexpr int KQ = (L + 2 + 15) / 16;
+    const uint32_t rows = nenv * (uint32_t)na, tiles = (rows + 31u) / 32u;   // (a tail group: fewer)
+    uint4* out = xfrag + ((e0 * na) / 32) * (int64_t)(KQ * 64);
+    for (uint32_t c = tid; c < tiles * KQ * 64; c += BT) {
+      const uint32_t lane = c & 63u, tq = c >> 6, q = tq % KQ, t = tq / KQ;
+      const uint32_t row = t * 32u + (lane & 31u);   // counted from the group's first env
+      const uint32_t el1 = row / (uint32_t)na, i = row - el1 * (uint32_t)na;
+      const bool rl = row < rows;
+      const uint32_t lim = rl ? O.lim[el1] : 0u;
+      const bool live_row = rl && i < ((lim & 0x7FFFFFFFu) / L);
+      const uint8_t* sb = reinterpret_cast<const uint8_t*>(O.src[lim >> 31]);
+      const uint8_t* im = O.img[rl ? el1 : 0];
+      uint32_t w[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        uint32_t hv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t k = 16u * q + 8u * (lane >> 5) + 2u * jj + u;
+          float v = 0.0f;
+          if (k < (uint32_t)L) v = live_row ? (float)im[sb[i * L + k]] : 0.0f;
+          else if (k < (uint32_t)L + 2u) v = 1.0f;
+          hv[u] = __float_as_uint(v) >> 16;   // byte values and 1.0: exact in bf16
+        }
+        w[jj] = hv[0] | (hv[1] << 16);
+      }
+      out[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  if (!obs) return;
   float* out = obs + e0 * per_env;
   if (quads) {
     // per_env % 4 == 0 and obs 16-byte aligned (checked on the host)
@@ -1605,7 +1643,7 @@ struct Kernels {
   void (*step_fast[3])(StepParams);   // [policy]: greedy / random fused rollouts (NAM even), else null
   void (*step_ordered)(StepParams);
   void (*reset)(ResetParams);
-  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int);   // 8 / 16 / 64 envs per WG
+  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // 8 / 16 / 64 envs per WG
   int tblw, nv;
 };
 
@@ -1941,23 +1979,33 @@ int wh_launch_run_timed(const wh_launch* l, void* start_event, void* stop_event)
 
 void wh_launch_free(wh_launch* l) { delete l; }
 
-int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* stream) {
+static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* xfrag,
+                        void* stream) {
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
   int rc = prepare(cfg, B, stream, &g, &k, &tab);
   if (rc) return rc;
   if (B == 0) return WH_OK;
-  if (!state || !obs) return WH_EINVAL;
+  if (!state || (!obs && !xfrag)) return WH_EINVAL;
   const int quads = ((g.NA * (9 * g.R + 1)) % 4 == 0) && ((uintptr_t)obs % 16 == 0);
   // envs per workgroup: ~40-75 KB of rows per group (measured: 64 for Small-4's 592 B/env rows,
   // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
   const int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
   const int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
+  if (xfrag && ((ebx * g.NA) % 32 != 0 || (uintptr_t)xfrag % 16 != 0)) return WH_ENOTSUP;
   hipLaunchKernelGGL(k->observe[sel], dim3((unsigned)((B + ebx - 1) / ebx)), dim3(BT), 0,
-                     (hipStream_t)stream, state, B, g.NA, tab, obs, quads);
+                     (hipStream_t)stream, state, B, g.NA, tab, obs, quads, static_cast<uint4*>(xfrag));
   return hip_err(hipGetLastError());
+}
+
+int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* stream) {
+  return observe_impl(cfg, B, state, obs, nullptr, stream);
+}
+
+int wh_observe_x(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* xfrag, void* stream) {
+  return observe_impl(cfg, B, state, obs, xfrag, stream);
 }
 
 int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,

@@ -32,6 +32,7 @@ WH_POLICY_RANDOM = 2
 # every symbol include/warehouse_amd.h declares
 SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observe", "wh_policy",
            "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version",
+           "wh_observe_x", "wh_mlp_forward_x",
            "wh_check_read", "wh_rollout_prepare", "wh_launch_run", "wh_launch_run_timed", "wh_launch_free")
 
 
@@ -114,6 +115,7 @@ def lib() -> ctypes.CDLL:
     L.wh_reset.argtypes = [_CFG, _I64, _P, _P, ctypes.POINTER(WhResetDraws), _I32, _U64, _I64, _P]
     L.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P]
     L.wh_observe.argtypes = [_CFG, _I64, _P, _P, _P]
+    L.wh_observe_x.argtypes = [_CFG, _I64, _P, _P, _P, _P]
     L.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
     _ST = ctypes.POINTER(WhEpisodeStats)
     L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
@@ -122,6 +124,7 @@ def lib() -> ctypes.CDLL:
     L.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
     L.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
     L.wh_mlp_forward.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
+    L.wh_mlp_forward_x.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
     L.wh_check_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), _I32]
     L.wh_rollout_prepare.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P,
                                      ctypes.POINTER(ctypes.c_void_p)]

@@ -203,6 +203,21 @@ class BatchedWarehouse:
         self._call("wh_observe", self.state.data_ptr(), self._obs.data_ptr(), self.stream)
         return self._obs
 
+    def observe_x(self, obs: bool = False):
+        """The observation rows as the policy network's layer-0 operand (wh_observe_x: bf16, MFMA
+        fragment order, for MLPPolicy.forward_x), optionally also the f32 rows.  Returns the
+        env-owned uint8 buffer [tiles, KQ, 64, 16] (and the obs tensor when obs=True)."""
+        kq = (self.obs_len + 2 + 15) // 16
+        tiles = (self.B * self.agent_slots + 31) // 32
+        if getattr(self, "_xfrag", None) is None or self._xfrag.shape[0] != tiles:
+            self._xfrag = torch.empty((tiles, kq, 64, 16), dtype=torch.uint8, device=self.device)
+        if obs and self._obs is None:
+            self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
+                                    device=self.device)
+        self._call("wh_observe_x", self.state.data_ptr(), self._obs.data_ptr() if obs else None,
+                   self._xfrag.data_ptr(), self.stream)
+        return (self._xfrag, self._obs) if obs else self._xfrag
+
     def vector_step(self, actions, autoreset: bool = True, observe: bool = True, mask=None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
         """Sampler step (wh_vector_step): step every env (or those in the [B] bool `mask`) with

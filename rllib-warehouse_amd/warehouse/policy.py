@@ -92,6 +92,26 @@ class MLPPolicy:
 
     __call__ = forward
 
+    def forward_x(self, xfrag: torch.Tensor, rows: int, *, explore: bool = False, seed: int = 0,
+                  step: Optional[int] = None, actions: Optional[torch.Tensor] = None,
+                  logits: Optional[torch.Tensor] = None):
+        """forward() on BatchedWarehouse.observe_x()'s fragment-order operand (rows = B x NA agent
+        rows; bf16 precision only): the same actions/logits as forward() on the f32 rows."""
+        if self.precision != "bf16":
+            raise ValueError("forward_x needs precision='bf16'")
+        if actions is None:
+            actions = torch.empty(rows, dtype=torch.int32, device=self.device)
+        if logits is True:
+            logits = torch.empty((rows, NUM_ACTIONS), dtype=torch.float32, device=self.device)
+        if step is None:
+            step, self._step = self._step, self._step + 1
+        nat.check(nat.lib().wh_mlp_forward_x(ctypes.byref(self.desc), self.packed.data_ptr(), int(rows),
+                                             xfrag.data_ptr(),
+                                             nat.ptr(logits if logits is not None and logits is not False else None),
+                                             actions.data_ptr(), int(bool(explore)), int(seed), int(step) & 0xFFFFFFFF,
+                                             nat.stream_of(self.device)), "wh_mlp_forward_x")
+        return actions, (logits if torch.is_tensor(logits) else None)
+
 
 def policy_rollout(env, net: MLPPolicy, steps: int, *, explore: bool = False, seed: int = 0,
                    first_step: int = 0, record=None):

@@ -193,3 +193,50 @@ def test_mlp_f32_edge_cases(wh):
         assert np.abs(lg.cpu().numpy() - ref).max() <= 1e-5 * np.abs(ref).max()
     with pytest.raises(ValueError):
         wh.policy.MLPPolicy("medium", precision="fp16")
+
+
+def frag_reference(rows_f32, kq):
+    """numpy: f32 rows [N, L] -> wh_observe_x's layout [tiles, kq, 64 lanes, 8] bf16 bits."""
+    import torch
+
+    N, L = rows_f32.shape
+    tiles = (N + 31) // 32
+    X = np.zeros((tiles * 32, 16 * kq), np.float32)
+    X[:N, :L] = rows_f32
+    X[:, L:L + 2] = 1.0
+    bits = torch.as_tensor(X).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    out = np.zeros((tiles, kq, 64, 8), np.uint16)
+    for h in range(2):
+        for q in range(kq):
+            out[:, q, 32 * h:32 * h + 32, :] = bits.reshape(tiles, 32, 16 * kq)[:, :, 16 * q + 8 * h:16 * q + 8 * h + 8]
+    return out
+
+
+@pytest.mark.parametrize("variant,na,B", [("small", 4, 100), ("medium", 8, 61), ("large", 16, 37)])
+def test_observe_x_fragments_and_forward_x(wh, variant, na, B):
+    """wh_observe_x writes exactly the bf16 fragment image of wh_observe's rows (bias columns 1.0,
+    padding 0, ragged last tile), and wh_mlp_forward_x on it gives bit-identical logits and actions
+    to wh_mlp_forward on the f32 rows (the kernel rounds those to bf16 the same way)."""
+    import torch
+
+    env = wh.BatchedWarehouse(variant, B, na, seed=8)
+    env.reset()
+    env.rollout(31, "greedy", 0.1)
+    xf, obs = env.observe_x(obs=True)
+    rows = obs.reshape(-1, env.obs_len)
+    kq = (env.obs_len + 2 + 15) // 16
+    ref = frag_reference(rows.cpu().numpy(), kq)
+    got = xf.cpu().numpy().view(np.uint16).reshape(ref.shape)
+    real = np.zeros(ref.shape[:1] + (32,), bool)
+    real.reshape(-1)[:rows.shape[0]] = True
+    for q in range(kq):        # rows past B*NA: not compared (never emitted by the MLP)
+        for h in range(2):
+            np.testing.assert_array_equal(got[:, q, 32 * h:32 * h + 32][real], ref[:, q, 32 * h:32 * h + 32][real])
+    np.testing.assert_array_equal(env.observe().cpu().numpy(), obs.cpu().numpy())
+    net = wh.policy.MLPPolicy(variant, seed=13)
+    a1, l1 = net(rows, logits=True, step=0)
+    a2, l2 = net.forward_x(xf, rows.shape[0], logits=True, step=0)
+    assert torch.equal(l1, l2) and torch.equal(a1, a2)
+    a3, _ = net(rows, explore=True, seed=5, step=9)
+    a4, _ = net.forward_x(xf, rows.shape[0], explore=True, seed=5, step=9)
+    assert torch.equal(a3, a4)
