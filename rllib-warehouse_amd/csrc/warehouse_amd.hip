@@ -442,6 +442,65 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
   s.epi = ep;
 }
 
+// The same philox reset for ONE env -- the env of lane l of this wave -- computed by the whole
+// wave: a Philox block per lane (lane b holds block b), words read across lanes, the subset and
+// target arithmetic on wave-uniform values (target ranks by v_mbcnt + ballot), and lane l's LDS
+// column (pickup cells, occupancy rows) written one cell per lane.  Bit-identical to
+// reset_philox<C, NA> (plus the occupancy clear) for that env, at a fraction of its issue cost:
+// the fused rollout uses it when a single lane of the wave ends its episode, which is what
+// desynchronised episodes produce (env ends are spread over the steps, B/T per step).
+template <class C, int NA>
+__device__ __forceinline__ void reset_lane(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
+                                           int variable_n, uint32_t W, int tid, int l) {
+  const int lane = tid & 63;
+  const int col = (tid & ~63) + l;                      // lane l's LDS column
+  const uint32_t me = mask_z((uint32_t)(lane ^ l));      // all-ones on lane l
+  const uint32_t gid_l = __builtin_amdgcn_readlane(gid, l);
+  const uint32_t ep = __builtin_amdgcn_readlane(s.epi, l) + 1u;
+  constexpr int NB = (1 + NA + 2 * C::R + 3) / 4;
+  static_assert(NB <= 64, "one Philox block per lane");
+  const uint4 mine = stream_block(k, gid_l, ep, 0u, PUR_RESET, (uint32_t)(lane < NB ? lane : 0));
+  auto word = [&](int j) -> uint32_t { return __builtin_amdgcn_readlane(comp(mine, j & 3), j >> 2); };
+  const uint32_t n = variable_n ? 1u + __umulhi(word(0), (uint32_t)NA) : (uint32_t)NA;
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i) {
+    uint32_t a = IDLE;
+    if (i < NA) {
+      const uint32_t v = __umulhi(word(1 + i), (uint32_t)C::NV);
+      a = (i < (int)n) ? (L.valid_cell(v) | IDLE) : IDLE;
+    }
+    s.ag[i] = msel(me, a, s.ag[i]);
+  }
+  if (lane < C::P) L.pkp[lane][col] = 0;
+  if (lane < C::D) L.occ[lane][col] = 0u;
+  const uint32_t wexp = (W & 0xFFu) << 8;
+  // points: Floyd's subset on wave-uniform values (a short scalar chain); lane j < R keeps item j
+  uint64_t S = 0;
+  uint32_t selv = (uint32_t)C::P, tgv = 0;
+#pragma unroll
+  for (int j = 0; j < C::R; ++j) {
+    const uint32_t m = (uint32_t)(C::P - C::R + j);
+    const uint32_t r = __umulhi(word(1 + NA + 2 * j), m + 1u);
+    const uint32_t sel = (j > 0 && ((S >> r) & 1ull)) ? m : r;
+    S |= 1ull << sel;
+    selv = lane == j ? sel : selv;
+    tgv = lane == j ? __umulhi(word(2 + NA + 2 * j), (uint32_t)(C::DP - j)) : tgv;   // rank r2_j
+  }
+  // targets: item j is the r2_j-th delivery point not taken by items < j.  Decoded in parallel
+  // (lane j holds item j): from the last item back, every later item at or above item j's value
+  // moves up one -- the same values as the per-lane rank selection, without its serial chain.
+#pragma unroll
+  for (int j = C::R - 2; j >= 0; --j) {
+    const uint32_t xj = __builtin_amdgcn_readlane(tgv, j);
+    tgv += (lane > j && lane < C::R && tgv >= xj) ? 1u : 0u;
+  }
+  const uint32_t valv = (tgv + 1u) | wexp;
+  if (lane < C::R) L.pkp[selv][col] = (uint16_t)valv;     // after the clear (LDS ops in order)
+  s.am = ((uint64_t)msel(me, (uint32_t)(S >> 32), (uint32_t)(s.am >> 32)) << 32) | msel(me, (uint32_t)S, (uint32_t)s.am);
+  s.hdr = msel(me, (n << 16) | (1u << 24), s.hdr);
+  s.epi = msel(me, ep, s.epi);
+}
+
 template <class C>
 __device__ __forceinline__ void reset_injected(Regs<C>& s, Lds<C>& L, int64_t e, int na,
                                                const int32_t* spawn, const int32_t* pickups,
@@ -595,7 +654,18 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     //      requests, so the two commute, and the pickup table is final before the move loop --
     //      which lets its lookups be issued inside it.
     WH_PHASE_MARK(expire);
-    if (!(ablate & 4) && __any(t >= s.wskip)) {
+    const uint64_t em = (ablate & 4) ? 0ull : __ballot(t >= s.wskip);
+    if (em && __popcll(em) == 1 && __ballot(true) == ~0ull) {
+      // one lane of a full wave due (desynchronised episodes): its P pickup cells checked one per
+      // lane of the wave, instead of the whole wave walking every lane's requests
+      const int l = __builtin_ctzll(em), lane = tid & 63, col = (tid & ~63) + l;
+      const uint32_t t8 = (uint32_t)__builtin_amdgcn_readlane(t, l) & 0xFFu;
+      const uint32_t v = lane < C::P ? (uint32_t)L.pkp[lane][col] : 0u;
+      const bool ex = (v & 0xFFu) != 0u && (v >> 8) == t8;
+      if (ex) L.clear_target(lane, col);
+      const uint64_t exm = __ballot(ex);
+      s.am = lane == l ? (s.am & ~exm) : s.am;
+    } else if (em) {
       if (__any(__popcll(s.am) > C::R)) {   // a hand-built state with more than R requests: scan all
         uint64_t expired = 0;
 #pragma unroll
@@ -782,7 +852,11 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   if (!(ablate & 16)) {
     const uint64_t inactive = ~s.am & low_mask<C::P>();
     const uint32_t nin = (uint32_t)__popcll(inactive);
-    const int kreq = C::R - C::P + (int)nin;
+    // The fused rollout (INJ = false) always auto-resets a finished episode, and a regeneration
+    // at its last step (t = T) lands in state the reset replaces: skipped.  (With desynchronised
+    // episodes that step's expiry makes it the deepest regeneration of the episode, and the whole
+    // wave would walk it for one lane.)
+    const int kreq = (!INJ && t >= T) ? 0 : C::R - C::P + (int)nin;
     if (phase == PH_PRE) {
       if (n_inactive) n_inactive[e] = (int32_t)nin;
     } else {
@@ -1126,7 +1200,16 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
     rrow += rstride;
     drow += a.B;
     if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
-      if (done) {
+      const uint64_t dm = __ballot(done);
+      // one env of a full wave ends (desynchronised episodes): a wave-wide reset of it (every lane
+      // takes part, so not in a tail wave whose lanes past B have exited)
+#ifndef WH_NO_LANE_RESET   // (A/B builds: tools/build_variant.sh nolane -DWH_NO_LANE_RESET)
+      if (__popcll(dm) == 1 && __ballot(true) == ~0ull) {
+#else
+      if (false) {
+#endif
+        reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+      } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;

@@ -1,0 +1,7 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+bash tools/gpu_round.sh \
+  "python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread" \
+  "python bench.py --gpus 1 --steps 20 --warmup 5 --no-alt --no-sampler --no-policy --no-cpu-baseline" \
+  "python bench.py --gpus 1 --steps 20 --warmup 5 --no-alt --no-sampler --no-policy --no-cpu-baseline" \
+  "python bench.py --gpus 1 --steps 200 --warmup 20 --no-alt --no-sampler --no-policy --no-cpu-baseline"
