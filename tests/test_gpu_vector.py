@@ -181,21 +181,24 @@ def test_base_env_poll_send_try_reset(wh):
         be.send_actions({0: {"0": 9}})
 
 
-@pytest.mark.parametrize("variant,na", [("medium", 8), ("large", 16)])
-def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na):
+@pytest.mark.parametrize("variant,na,train", [("medium", 8, False), ("large", 16, False), ("large", 16, True),
+                                              ("small", 4, True)])
+def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na, train):
     """Desynchronised episodes (BatchedWarehouse.stagger: env e takes e*7 % 200 extra masked greedy
     steps), then a 260-step fused rollout: every step some envs end, reset and run the expiry pass
-    while their wave-mates do not.  Rewards and dones every step, and the final state, equal the
-    oracle's (philox draws, auto-reset per env)."""
+    while their wave-mates do not (one env per wave: the wave-wide single-env reset and expiry).
+    Train variants redraw n at every reset.  Rewards and dones every step, and the final state,
+    equal the oracle's (philox draws, auto-reset per env)."""
     import torch
 
     B, seed, K = 1024, 13, 260
     L = oc.layout_for(variant)
-    env = wh.BatchedWarehouse(variant, B, na, seed=seed)
+    nmax = na if train else None
+    env = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
     env.reset()
     S = ob.BState.zeros(L, B, na)
     ids = np.arange(B)
-    ob.reset(L, S, ob.PhiloxDraws(seed, ids))
+    ob.reset(L, S, ob.PhiloxDraws(seed, ids), nmax=nmax)
     off = (ids * 7) % 200
     env.stagger(off)
     for s in range(int(off.max())):
@@ -204,7 +207,7 @@ def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na):
         d = ob.PhiloxDraws(seed, idx)
         _, odone, _, _ = ob.step(L, sub, ob.greedy(L, sub, 0.0, d), d)
         if odone.any():
-            ob.reset(L, sub, d, mask=odone)
+            ob.reset(L, sub, d, mask=odone, nmax=nmax)
         put(S, idx, sub)
     assert len(np.unique(S.t)) > 150                       # episode clocks are spread out
     rew = torch.zeros((K, B, na), device=env.device)
@@ -218,9 +221,10 @@ def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na):
         np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
         ends += int(odone.sum())
         if odone.any():
-            ob.reset(L, S, d, mask=odone)
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
     assert ends >= B                                        # every env crossed an episode end
     c = {k: v.cpu().numpy() for k, v in env.to_canonical().items()}
     np.testing.assert_array_equal(c["pos"], S.pos)
     np.testing.assert_array_equal(c["pickup_target"], S.pk_tgt)
     np.testing.assert_array_equal(c["t"], S.t)
+    np.testing.assert_array_equal(c["n"], S.n)
