@@ -385,6 +385,7 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 template <class C, int NAC = -1>
 __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
                                              int na_rt, int variable_n, uint32_t W, int tid) {
+  WH_PHASE_MARK(reset);
   const uint32_t ep = s.epi + 1u;
   const int na = NAC >= 0 ? NAC : na_rt;
   constexpr int NB = NAC >= 0 ? (1 + NAC + 2 * C::R + 3) / 4 : 1;
@@ -413,33 +414,35 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
   for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
   const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
   uint32_t plo = 0, phi = 0;                // Floyd's subset so far
-  uint64_t remD = low_mask<C::DP>();
-  uint32_t t0 = 0;
+  uint32_t sel[C::R], tg[C::R];
 #pragma unroll
   for (int j = 0; j < C::R; ++j) {
     constexpr int M0 = C::P - C::R;
     const uint32_t m = (uint32_t)(M0 + j);
     const uint32_t r = __umulhi(word(1 + na + 2 * j), m + 1u);
-    uint32_t sel = r;
+    sel[j] = r;
     if (j > 0) {   // taken already: bit r of the subset, moved to bit 63 by one 64-bit shift
       const uint64_t sh = (((uint64_t)phi << 32) | plo) << (63u - r);
-      sel = msel(sgn((uint32_t)(sh >> 32)), m, r);
+      sel[j] = msel(sgn((uint32_t)(sh >> 32)), m, r);
     }
-    const uint64_t sb = 1ull << sel;
+    const uint64_t sb = 1ull << sel[j];
     plo |= (uint32_t)sb;
     phi |= (uint32_t)(sb >> 32);
-    const uint32_t r2 = __umulhi(word(2 + na + 2 * j), (uint32_t)(C::DP - j));
-    uint32_t tg;
-    if (j == 0) tg = r2;
-    else if (j == 1) tg = r2 + ((t0 - 1u - r2) >> 31);   // + (r2 >= first): skip it
-    else tg = select_bit64(remD, r2);
-    if (j == 0) t0 = r2;
-    remD &= ~(1ull << tg);
-    L.pkp[sel][tid] = (uint16_t)((tg + 1u) | wexp);
+    tg[j] = __umulhi(word(2 + na + 2 * j), (uint32_t)(C::DP - j));   // rank among unused targets
   }
+  // ranks -> targets (item j: the tg[j]-th delivery point not taken by items < j), decoded from
+  // the last item back: every later item at or above item j's value moves up one.  The same
+  // values as a rank selection per item, as independent compare-adds instead of a serial chain.
+#pragma unroll
+  for (int j = C::R - 2; j >= 0; --j)
+#pragma unroll
+    for (int i = j + 1; i < C::R; ++i) tg[i] += 1u - ((tg[i] - tg[j]) >> 31);   // + (tg[i] >= tg[j])
+#pragma unroll
+  for (int j = 0; j < C::R; ++j) L.pkp[sel[j]][tid] = (uint16_t)((tg[j] + 1u) | wexp);
   s.am = ((uint64_t)phi << 32) | plo;
   s.hdr = (n << 16) | (1u << 24);
   s.epi = ep;
+  WH_PHASE_MARK(reset_end);
 }
 
 // The same philox reset for ONE env -- the env of lane l of this wave -- computed by the whole
@@ -452,6 +455,7 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
 template <class C, int NA>
 __device__ __forceinline__ void reset_lane(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
                                            int variable_n, uint32_t W, int tid, int l) {
+  WH_PHASE_MARK(lane_reset);
   const int lane = tid & 63;
   const int col = (tid & ~63) + l;                      // lane l's LDS column
   const uint32_t me = mask_z((uint32_t)(lane ^ l));      // all-ones on lane l

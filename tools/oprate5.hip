@@ -33,6 +33,8 @@ KERN(readlane, "v_readlane_b32 s2, %0, 0\n", : "s2")
 KERN(pkmin, "v_pk_min_i16 %0, %1, %2\n", )
 KERN(bfei, "v_bfe_i32 %0, %1, %2, 1\n", )
 KERN(mulhi, "v_mul_hi_u32 %0, %1, %2\n", )
+KERN(mullo, "v_mul_lo_u32 %0, %1, %2\n", )
+KERN(mul24, "v_mul_u32_u24 %0, %1, %2\n", )
 #define CL_MAD : "v2", "v3", "s2", "s3"
 KERN(madu64, "v_mad_u64_u32 v[2:3], s[2:3], %1, %2, 0\n", CL_MAD)
 
@@ -44,7 +46,8 @@ int main() {
       {"+ s_cmp; cbranch_scc0 nt", k_scmp_br}, {"+ v_ffbl", k_ffbl}, {"+ v_sad_hi_u8", k_sad},
       {"+ v_dot2c_i32_i16", k_dot2}, {"+ s_nop 0", k_nop},
       {"+ v_readlane", k_readlane}, {"+ v_pk_min_i16", k_pkmin}, {"+ v_bfe_i32", k_bfei},
-      {"+ v_mul_hi_u32", k_mulhi}, {"+ v_mad_u64_u32", k_madu64}};
+      {"+ v_mul_hi_u32", k_mulhi}, {"+ v_mul_lo_u32", k_mullo}, {"+ v_mul_u32_u24", k_mul24},
+      {"+ v_mad_u64_u32", k_madu64}};
   uint32_t* out;
   (void)hipMalloc(&out, 1024 * 256 * 4);
   hipEvent_t e0, e1;
