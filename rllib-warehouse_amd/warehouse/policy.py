@@ -114,18 +114,31 @@ class MLPPolicy:
 
 
 def policy_rollout(env, net: MLPPolicy, steps: int, *, explore: bool = False, seed: int = 0,
-                   first_step: int = 0, record=None):
+                   first_step: int = 0, record=None, operand: str = "auto"):
     """scripts/rollout.py's loop (compute_action per agent -> env.step, until done) for every env
-    of a BatchedWarehouse, on the device: per step one wh_mlp_forward over all B x NA observation
-    rows, then one wh_vector_step (step + auto-reset + the next observation rows).  `record`, if
-    given, is called as record(step, actions, rewards, dones) with env-owned device tensors.
-    Returns the obs tensor of the last step."""
-    obs = env.observe()
+    of a BatchedWarehouse, on the device: per step one network forward over all B x NA observation
+    rows, then one wh_vector_step (step + auto-reset) and the next rows.  operand="fragments" (the
+    default for bf16 networks) hands the rows to the network as its layer-0 operand
+    (wh_observe_x / wh_mlp_forward_x: the same actions, no f32 rows materialised); "rows" uses the
+    float32 observation rows.  `record`, if given, is called as record(step, actions, rewards,
+    dones) with env-owned device tensors.  Returns the last step's observations (the fragment
+    buffer or the obs tensor)."""
+    if operand == "auto":
+        operand = "fragments" if net.precision == "bf16" else "rows"
+    if operand not in ("fragments", "rows"):
+        raise ValueError("operand must be 'auto', 'fragments' or 'rows'")
     B, NA = env.B, env.agent_slots
     acts = torch.empty((B, NA), dtype=torch.int32, device=env.device)
+    frag = operand == "fragments"
+    obs = env.observe_x() if frag else env.observe()
     for s in range(steps):
-        net(obs.view(B * NA, -1), explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
-        obs, rew, done = env.vector_step(acts, autoreset=True, observe=True)
+        if frag:
+            net.forward_x(obs, B * NA, explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
+            _, rew, done = env.vector_step(acts, autoreset=True, observe=False)
+            obs = env.observe_x()
+        else:
+            net(obs.view(B * NA, -1), explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
+            obs, rew, done = env.vector_step(acts, autoreset=True, observe=True)
         if record is not None:
             record(s, acts, rew, done)
     return obs

@@ -117,10 +117,11 @@ def test_mlp_edge_cases(wh):
                                     None, 0, 0, 0, None) == nat.WH_ENOTSUP
 
 
-def test_policy_rollout_transitions_vs_oracle(wh):
-    """The device policy loop (wh_mlp_forward -> wh_vector_step with auto-reset) for 230 steps:
-    actions equal a separate forward on the same rows, and every transition equals the oracle's
-    given those actions (philox draws)."""
+@pytest.mark.parametrize("operand", ["fragments", "rows"])
+def test_policy_rollout_transitions_vs_oracle(wh, operand):
+    """The device policy loop (network forward -> wh_vector_step with auto-reset) for 230 steps, on
+    the fragment-order operand and on the f32 rows: actions equal a separate forward on the same
+    rows, and every transition equals the oracle's given those actions (philox draws)."""
     import torch
 
     from oracle import batched as ob
@@ -141,7 +142,7 @@ def test_policy_rollout_transitions_vs_oracle(wh):
 
     obs0 = env.observe().clone()
     ref_a0, _ = net(obs0.view(B * na, -1), explore=True, seed=1, step=0)
-    wh.policy.policy_rollout(env, net, 230, explore=True, seed=1, record=record)
+    wh.policy.policy_rollout(env, net, 230, explore=True, seed=1, record=record, operand=operand)
     np.testing.assert_array_equal(log[0][0].reshape(-1), ref_a0.cpu().numpy())
     for s, (a, rew, done) in enumerate(log):
         orew, odone, _, _ = ob.step(L, S, a, d)
