@@ -632,14 +632,19 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
 // always draw from philox): less code in the step loop and no per-step test of `regen`.
 // CLAMP = false: the steps come from the greedy policy, whose goals are grid cells, so pos + d
 // never leaves the grid and the off-grid rule (a clamp) is the identity.
-template <class C, bool ORDERED, bool INJ = true, bool CLAMP = true>
+struct LazyGrid {
+  bool rebuild;   // the occupancy grid may lack an agent's cell: rebuild it before the next move
+  uint32_t cm;    // slots sharing a cell (found by the last rebuild or reset): rebuild once one moves
+};
+
+template <class C, bool ORDERED, bool INJ = true, bool CLAMP = true, bool LAZY = false>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
                                          const int32_t* __restrict__ actions_g,
                                          const int32_t* __restrict__ regen, const Keys& k,
                                          uint32_t gid, int64_t e, int na, int phase, uint32_t T,
                                          uint32_t W, float (&rew)[C::NAM], int32_t* n_inactive,
-                                         int tid, int ablate) {
+                                         int tid, int ablate, LazyGrid* lg = nullptr) {
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   uint32_t t = s.hdr & 0xFFFFu;
   uint32_t rewm[C::NAM];   // reward masks: all-ones = 1.0f
@@ -717,15 +722,54 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       // what the previous step left, which is always a subset of them (a set bit is an arrival
       // or an agent that stayed; leaving clears), so no per-step clear is needed.  k_step clears
       // it at launch and after an auto-reset; the ordered (drop-in) path clears it every step.
+      // LAZY (fused rollout): once rebuilt, the grid a lane carries stays exactly its agents' cells
+      // (a move is accepted only into a free cell) until an agent leaves a cell it shares -- the
+      // reference clears the cell under the agent that stays (core.py:290), and only its per-step
+      // rebuild sets it again.  Shared cells come from resets, whose spawns are drawn independently
+      // (core.py:191-201), and persist only while the agents sharing them stay put.  So a lane asks
+      // for the rebuild (lg->rebuild) after a grid clear, and after a step in which an agent that
+      // shares a cell (lg->cm) moved; the wave skips it when no lane asks.
       if (ORDERED) {
 #pragma unroll
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
       }
+      if (!LAZY) {
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) {
-        const uint32_t p = s.ag[i] & XY16;
-        const uint32_t mlive = sgn((uint32_t)i - n);
-        atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
+        for (int i = 0; i < C::NAM; ++i) {
+          const uint32_t p = s.ag[i] & XY16;
+          const uint32_t mlive = sgn((uint32_t)i - n);
+          atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
+        }
+      } else if (__any(lg->rebuild)) {
+        // (the terms are written so that none is shared with the move loop below: a shared one
+        // would be hoisted above the branch, and the skip path would pay a register copy per term)
+        const uint32_t livebits = (2u << (n - 1u)) - 1u;   // n >= 1
+        uint32_t q[C::NAM];   // live cells; slots >= n get distinct off-grid stand-ins
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) {
+          const uint32_t a = s.ag[i];
+          const uint32_t mlive = (uint32_t)__builtin_amdgcn_sbfe((int)livebits, (uint32_t)i, 1u);
+          uint32_t bit;
+          asm volatile("v_lshlrev_b32 %0, %1, 1" : "=v"(bit) : "v"(a));   // 1 << (x & 31)
+          atomicOr(&L.occ[__builtin_amdgcn_ubfe(a, 16u, 8u)][tid], bop3<TA & TB>(mlive, bit, 0u));
+          q[i] = msel(mlive, a, 0x80u + (uint32_t)i);   // position bytes compared below
+        }
+        uint32_t m[C::NAM];   // m[i] == 0: slot i shares its cell
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) m[i] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 1; i < C::NAM; ++i)
+#pragma unroll
+          for (int j = 0; j < i; ++j) {
+            const uint32_t x = bop3<(TA ^ TB) & TC>(q[i], q[j], XY16);
+            m[i] = min(m[i], x);
+            m[j] = min(m[j], x);
+          }
+        uint32_t cm = 0;
+#pragma unroll
+        for (int i = 0; i < C::NAM; ++i) cm |= (m[i] == 0u ? 1u : 0u) << i;
+        lg->cm = cm;
+        lg->rebuild = false;
       }
       // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
       uint32_t kk[3 * C::NAM];   // ORDERED path: 3 ordered keys per accepted move
@@ -817,6 +861,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
         dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
         looked = true;
+        if (LAZY && __any(lg->cm != 0u)) {   // did an agent that shares a cell move?
+          uint32_t acc = 0;
+#pragma unroll
+          for (int i = 0; i < C::NAM; ++i)
+            acc |= (s.ag[i] ^ pp[i]) & (XY16 & (uint32_t)__builtin_amdgcn_sbfe((int)lg->cm, (uint32_t)i, 1u));
+          lg->rebuild = lg->rebuild || acc != 0u;
+        }
       }
     }
 
@@ -1163,6 +1214,12 @@ __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C
 // rows).  No per-step tests of launch options, and the injected-draw path is compiled out, so a
 // step executes few branch instructions -- each costs several issue slots at one wave per SIMD
 // (tools/oprate5.hip: ~8 ns per s_cbranch/s_branch against ~2.6 ns per VALU op).
+#ifndef WH_EAGER_GRID   // (A/B builds: -DWH_EAGER_GRID rebuilds the grid every step)
+constexpr bool kLazyGrid = true;
+#else
+constexpr bool kLazyGrid = false;
+#endif
+
 template <class C>
 __device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]) {
   if constexpr ((C::NAM & 3) == 0) {
@@ -1186,6 +1243,7 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
   float* rrow = a.rewards + e * C::NAM;
   uint8_t* drow = a.dones + e;
   const int64_t rstride = a.B * C::NAM;
+  LazyGrid lg{true, 0u};   // the grid starts empty (k_step)
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t d[C::NAM];
     if (ablate & 1) {
@@ -1195,8 +1253,8 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
       policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
-                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate);
+    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg);
     if (!(ablate & 64)) {
       store_row<C>(rrow, rew);
       *drow = done ? 1 : 0;
@@ -1213,10 +1271,12 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
       if (false) {
 #endif
         reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+        lg.rebuild = lg.rebuild || done;   // its grid column was cleared
       } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
         for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+        lg.rebuild = true;
       }
     }
     WH_CHECK_ENV(s, L, e, tid);

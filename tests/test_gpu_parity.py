@@ -469,3 +469,41 @@ def test_timed_launch_equals_rollout_and_stamps_events(wh):
         spans[K] = e0.elapsed_time(e1)
         assert spans[K] > 0.0
     assert spans[60] > spans[5]
+
+
+@pytest.mark.parametrize("variant,na", [("medium", 8), ("large", 16)])
+def test_fast_rollout_co_located_agents_vs_oracle(wh, variant, na):
+    """The fast fused instance (rewards + dones, auto-reset) on states where agents share cells.
+    A co-located agent leaving clears the cell under the one that stays (core.py:289-291) until
+    the next step's rebuild (core.py:275-276); the fast instance rebuilds only for lanes whose
+    co-located agents moved, so this is its exactness case: up to half the agents start in pairs
+    on shared cells (pairs that stay put keep sharing), and the rollout crosses two episode ends
+    (fresh spawns share cells again)."""
+    import torch
+
+    B, seed, K = 2048, 17, 430
+    L = oc.layout_for(variant)
+    env = wh.BatchedWarehouse(variant, B, na, seed=seed)
+    env.reset()
+    env.rollout(13, "greedy", 0.0)
+    c = canon(env)
+    rng = np.random.RandomState(1)
+    pos = c["pos"].copy()
+    for e in range(B):
+        k = rng.randint(1, na // 2 + 1)                         # k pairs share a cell
+        slots = rng.permutation(na)[: 2 * k]
+        pos[e, slots[1::2]] = pos[e, slots[0::2]]
+    c["pos"] = pos
+    env.from_canonical(c)
+    S = oracle_state(canon(env), L)
+    rew = torch.zeros((K, B, na), device=env.device)
+    dn = torch.zeros((K, B), dtype=torch.uint8, device=env.device)
+    env.rollout(K, "greedy", 0.0, rewards=rew, dones=dn)
+    d = ob.PhiloxDraws(seed, np.arange(B))
+    for s in range(K):
+        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        np.testing.assert_array_equal(rew[s].cpu().numpy(), orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone)
+    assert_same(canon(env), S, "after rollout")

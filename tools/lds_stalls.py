@@ -29,7 +29,7 @@ def main():
     lines = open(path).read().split("\n")
     start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
     end = next(i for i in range(start, len(lines)) if "codeLenInByte" in lines[i])
-    heads = [i for i in range(start, end) if "This Loop Header: Depth=1" in lines[i]]
+    heads = [i for i in range(start, end) if "Loop Header: Depth=1" in lines[i]]
     lo = heads[-1]
     phase = "head"
     slots = 0

@@ -26,12 +26,15 @@ def main():
     ap.add_argument("--launches", type=int, default=6)
     ap.add_argument("--policy", default="greedy")
     ap.add_argument("--train", action="store_true")
+    ap.add_argument("--stagger", action="store_true", help="desynchronised episodes (bench.py's desync leg)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     env = warehouse.BatchedWarehouse(a.variant, a.envs, None if a.train else a.agents, train=a.train,
                                      seed=3, device=dev)
     env.reset()
+    if a.stagger:
+        env.stagger((torch.arange(a.envs, dtype=torch.int64) * 37) % 200)
     NA = env.agent_slots
     rew = torch.zeros((a.steps, a.envs, NA), device=dev)
     dn = torch.zeros((a.steps, a.envs), dtype=torch.uint8, device=dev)
