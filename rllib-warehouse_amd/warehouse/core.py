@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -88,10 +88,21 @@ class Warehouse(MultiAgentEnv):
         self._done = False
         self._prev = None          # host snapshot before the last step (core.py:270-272), kept
         self._rendering = False    # only once render() has been called: it costs a device copy
+        self._io = None            # per-step upload buffers, sized by num_agents (Train re-inits)
 
     # ------------------------------------------------------------------ helpers
-    def _obs_dicts(self) -> Dict[str, Dict[str, np.ndarray]]:
-        rows = self._engine.observe()[0].cpu().numpy().astype(np.int32)
+    def _io_buffers(self):
+        """Pinned host and device buffers for the per-step uploads (allocated on first step)."""
+        if self._io is None:
+            n, R, dev = self._num_agents, self._num_requests, self._engine.device
+            h_io = torch.empty((2, n), dtype=torch.int32).pin_memory()
+            h_regen = torch.empty((1, 2 * R), dtype=torch.int32).pin_memory()
+            self._io = (h_io, torch.empty_like(h_io, device=dev), h_regen, torch.empty_like(h_regen, device=dev))
+        return self._io
+
+    def _obs_dicts(self, rows: Optional[np.ndarray] = None) -> Dict[str, Dict[str, np.ndarray]]:
+        if rows is None:
+            rows = self._engine.observe()[0].cpu().numpy().astype(np.int32)
         R = self._num_requests
         out = {}
         for i in range(self._num_agents):
@@ -127,8 +138,10 @@ class Warehouse(MultiAgentEnv):
     def step(self, action_dict: Dict[str, int]
              ) -> Tuple[Dict[str, dict], Dict[str, float], Dict[str, bool], Dict[str, dict]]:
         n, R = self._num_agents, self._num_requests
-        order = np.full((1, n), -1, np.int32)
-        acts = np.full((1, n), 4, np.int32)
+        h_io, d_io, h_regen, d_regen = self._io_buffers()
+        io = h_io.numpy()                                    # row 0: actions, row 1: dict order
+        io[0] = 4
+        io[1] = -1
         for s, (key, action) in enumerate(action_dict.items()):
             idx = int(key)
             a = int(action)
@@ -136,23 +149,33 @@ class Warehouse(MultiAgentEnv):
                 raise IndexError("list index out of range")
             if not 0 <= idx < n:
                 raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
-            order[0, s] = idx
-            acts[0, idx] = a % 9                             # Python's negative-index wrap
+            io[1, s] = idx
+            io[0, idx] = a % 9                               # Python's negative-index wrap
         eng = self._engine
         if self._rendering:
             self._prev = self._snapshot()                    # core.py:270-272
-        eng.step(acts, order=order, phase=nat.WH_PHASE_PRE_REGEN)
+        # One step costs two host round trips: the reference draws the regeneration on the host
+        # from the post-pickup count of free points (core.py:339-350), so n_inactive must come
+        # back; then observations, rewards and dones come back in one copy.  Uploads are async
+        # from pinned buffers on the launch stream (each is rewritten only after a later sync).
+        d_io.copy_(h_io, non_blocking=True)
+        eng.step(d_io[0:1], order=d_io[1:2], phase=nat.WH_PHASE_PRE_REGEN)
         n_in = int(eng.n_inactive[0].item())
         k = R - self._num_pickup_points + n_in
         rpos = np.random.choice(n_in, k, replace=False)                       # core.py:339-343
         rtgt = np.random.choice(self._num_delivery_points, k, replace=False)  # core.py:346-350
-        regen = np.full((1, 2 * R), -1, np.int32)
+        regen = h_regen.numpy()
+        regen[:] = -1
         regen[0, :k] = rpos
         regen[0, R:R + k] = rtgt
-        eng.step(None, regen=regen, phase=nat.WH_PHASE_REGEN)
-        obs = self._obs_dicts()
-        rew = eng.rewards[0].cpu().numpy()
-        done = bool(eng.dones[0].item())
+        d_regen.copy_(h_regen, non_blocking=True)
+        eng.step(None, regen=d_regen, phase=nat.WH_PHASE_REGEN)
+        rows_d = eng.observe()[0]
+        packed = torch.cat((rows_d.reshape(-1), eng.rewards[0], eng.dones[:1].float())).cpu().numpy()
+        nrow = rows_d.numel()
+        obs = self._obs_dicts(packed[:nrow].reshape(rows_d.shape).astype(np.int32))
+        rew = packed[nrow:nrow + n]
+        done = bool(packed[-1])
         rewards = {str(i): rew[i] for i in range(n)}
         dones = {str(i): done for i in range(n)}
         dones["__all__"] = done

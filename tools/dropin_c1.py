@@ -7,7 +7,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "rllib-warehouse_amd")]
+sys.path[:0] = [ROOT, os.environ.get("WH_PKG_DIR", os.path.join(ROOT, "rllib-warehouse_amd"))]   # A/B: another package copy
 import numpy as np  # noqa: E402
 import warehouse  # noqa: E402
 
@@ -33,11 +33,18 @@ def greedy(obs, n, p, rng_draw):
     return acts
 
 
+EPISODES = int(os.environ.get("C1_EPISODES", "3"))
 np.random.seed(0)
 env = warehouse.WarehouseSmall(2)
+if os.environ.get("C1_WARM"):              # one untimed episode first (launch paths, pinned buffers)
+    obs, done = env.reset(), False
+    while not done:
+        obs, _, dones, _ = env.step(greedy(obs, 2, 0.0, np.random.uniform))
+        done = dones["__all__"]
+    np.random.seed(0)
 t0 = time.perf_counter()
 steps, total = 0, 0.0
-for ep in range(3):
+for ep in range(EPISODES):
     obs = env.reset()
     done = False
     while not done:
@@ -46,6 +53,7 @@ for ep in range(3):
         steps += 1
         done = dones["__all__"]
 dt = time.perf_counter() - t0
-print(json.dumps({"config": "C1: WarehouseSmall(2), greedy p=0, drop-in single env, 3 episodes",
-                  "episodes": 3, "steps": steps, "total_reward": total,
+print(json.dumps({"config": f"C1: WarehouseSmall(2), greedy p=0, drop-in single env, {EPISODES} episodes"
+                            + (" after a warm-up episode" if os.environ.get("C1_WARM") else ""),
+                  "episodes": EPISODES, "steps": steps, "total_reward": total,
                   "agent_steps_per_s": 2 * steps / dt, "wall_s": dt}), flush=True)
