@@ -135,16 +135,34 @@ class WarehouseBaseEnv:
         self._pending = self._pack(obs, None, None, range(self.num_envs))
 
     def _pack(self, obs, rew, done, env_ids):
-        n = ((self.vec.env.state[0] >> 16) & 0xFF).cpu().numpy()
-        o = obs.cpu().numpy()
-        r = None if rew is None else rew.cpu().numpy()
-        d = None if done is None else done.cpu().numpy()
+        # Only the rows of `env_ids` leave the device, gathered there and brought back in ONE
+        # download: [n | rewards | done | obs rows] as f32 per env (n <= 255 and done in {0, 1} are
+        # exact in f32).  try_reset of one env therefore copies one env's rows, not the batch's.
+        env_ids = list(env_ids)
+        if not env_ids:
+            return ({}, {}, {}, {}, {})
+        B, NA, L = obs.shape
+        sel = torch.as_tensor(env_ids, dtype=torch.long, device=obs.device)
+        cols = [((self.vec.env.state[0, sel] >> 16) & 0xFF).float()[:, None]]
+        if rew is not None:
+            cols.append(rew[sel].float())
+        if done is not None:
+            cols.append(done[sel].float()[:, None])
+        cols.append(obs[sel].reshape(len(env_ids), NA * L))
+        h = torch.cat(cols, 1).cpu().numpy()
+        n = h[:, 0].astype(np.int64)
+        c = 1
+        r = None if rew is None else h[:, c:c + NA]
+        c += 0 if rew is None else NA
+        d = None if done is None else h[:, c] != 0
+        c += 0 if done is None else 1
+        o = h[:, c:].reshape(len(env_ids), NA, L)
         res = ({}, {}, {}, {}, {})
-        for e in env_ids:
-            ids = [str(i) for i in range(int(n[e]))]
-            res[0][e] = {a: o[e, i] for i, a in enumerate(ids)}
-            res[1][e] = {a: (0.0 if r is None else float(r[e, i])) for i, a in enumerate(ids)}
-            dd = bool(d[e]) if d is not None else False
+        for k, e in enumerate(env_ids):
+            ids = [str(i) for i in range(int(n[k]))]
+            res[0][e] = {a: o[k, i] for i, a in enumerate(ids)}
+            res[1][e] = {a: (0.0 if r is None else float(r[k, i])) for i, a in enumerate(ids)}
+            dd = bool(d[k]) if d is not None else False
             res[2][e] = {**{a: dd for a in ids}, "__all__": dd}
             res[3][e] = {a: {} for a in ids}
             res[4][e] = {}
