@@ -157,13 +157,18 @@ class WarehouseBaseEnv:
         d = None if done is None else h[:, c] != 0
         c += 0 if done is None else 1
         o = h[:, c:].reshape(len(env_ids), NA, L)
+        agent_ids = [str(i) for i in range(NA)]
+        rl = None if r is None else r.tolist()
+        dl = [False] * len(env_ids) if d is None else d.tolist()
         res = ({}, {}, {}, {}, {})
         for k, e in enumerate(env_ids):
-            ids = [str(i) for i in range(int(n[k]))]
-            res[0][e] = {a: o[k, i] for i, a in enumerate(ids)}
-            res[1][e] = {a: (0.0 if r is None else float(r[k, i])) for i, a in enumerate(ids)}
-            dd = bool(d[k]) if d is not None else False
-            res[2][e] = {**{a: dd for a in ids}, "__all__": dd}
+            nk = int(n[k])
+            ids = agent_ids[:nk]
+            res[0][e] = dict(zip(ids, o[k, :nk]))
+            res[1][e] = dict.fromkeys(ids, 0.0) if rl is None else dict(zip(ids, rl[k][:nk]))
+            dd = dl[k]
+            res[2][e] = dict.fromkeys(ids, dd)
+            res[2][e]["__all__"] = dd
             res[3][e] = {a: {} for a in ids}
             res[4][e] = {}
         return res
