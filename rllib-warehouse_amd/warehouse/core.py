@@ -89,6 +89,18 @@ class Warehouse(MultiAgentEnv):
         self._prev = None          # host snapshot before the last step (core.py:270-272), kept
         self._rendering = False    # only once render() has been called: it costs a device copy
         self._io = None            # per-step upload buffers, sized by num_agents (Train re-inits)
+        # The engine's observation, reward and done buffers as views of ONE device block, so a step's
+        # results come back in a single download with no gather kernel (offsets 256-aligned: the
+        # kernels store rows with 16-byte writes).
+        eng = self._engine
+        o_bytes = 4 * self._num_agents * eng.obs_len
+        self._r_off = -(-o_bytes // 256) * 256
+        self._d_off = self._r_off + 256 * (-(-4 * self._num_agents // 256))
+        blob = torch.zeros(self._d_off + 256, dtype=torch.uint8, device=eng.device)
+        eng._obs = blob[:o_bytes].view(torch.float32).view(1, self._num_agents, eng.obs_len)
+        eng.rewards = blob[self._r_off:self._r_off + 4 * self._num_agents].view(torch.float32).view(1, self._num_agents)
+        eng.dones = blob[self._d_off:self._d_off + 1]
+        self._blob = blob
 
     # ------------------------------------------------------------------ helpers
     def _io_buffers(self):
@@ -170,12 +182,12 @@ class Warehouse(MultiAgentEnv):
         regen[0, R:R + k] = rtgt
         d_regen.copy_(h_regen, non_blocking=True)
         eng.step(None, regen=d_regen, phase=nat.WH_PHASE_REGEN)
-        rows_d = eng.observe()[0]
-        packed = torch.cat((rows_d.reshape(-1), eng.rewards[0], eng.dones[:1].float())).cpu().numpy()
-        nrow = rows_d.numel()
-        obs = self._obs_dicts(packed[:nrow].reshape(rows_d.shape).astype(np.int32))
-        rew = packed[nrow:nrow + n]
-        done = bool(packed[-1])
+        eng.observe()
+        h = self._blob.cpu().numpy()
+        L = eng.obs_len
+        obs = self._obs_dicts(h[:4 * n * L].view(np.float32).reshape(n, L).astype(np.int32))
+        rew = h[self._r_off:self._r_off + 4 * n].view(np.float32)
+        done = bool(h[self._d_off])
         rewards = {str(i): rew[i] for i in range(n)}
         dones = {str(i): done for i in range(n)}
         dones["__all__"] = done
