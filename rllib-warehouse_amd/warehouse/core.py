@@ -84,7 +84,8 @@ class Warehouse(MultiAgentEnv):
         self._engine = BatchedWarehouse(num_envs=1, num_agents=self._num_agents, geometry=geo,
                                         device=_default_device())
         w = {k: n for k, n in zip(OBS_KEYS, (1, R - 1, 2 * (R - 1), 2 * (R - 1), 4 * R, 1, 2, 2))}
-        self._obs_split = np.cumsum([w[k] for k in OBS_KEYS])[:-1]
+        ends = np.cumsum([w[k] for k in OBS_KEYS])
+        self._obs_slices = [slice(int(a), int(b)) for a, b in zip(np.r_[0, ends[:-1]], ends)]
         self._done = False
         self._prev = None          # host snapshot before the last step (core.py:270-272), kept
         self._rendering = False    # only once render() has been called: it costs a device copy
@@ -118,7 +119,8 @@ class Warehouse(MultiAgentEnv):
         R = self._num_requests
         out = {}
         for i in range(self._num_agents):
-            p = np.split(rows[i], self._obs_split)
+            row = rows[i]
+            p = [row[sl] for sl in self._obs_slices]
             out[str(i)] = {
                 "num_agents": p[0],
                 "self_position": p[7],

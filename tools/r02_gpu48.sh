@@ -1,5 +1,5 @@
 #!/bin/bash
-# drop-in outputs as views of one device block (no gather kernel): drop-in parity tests, then C1 A/B vs the cat+float version (old first) x3
+# drop-in C1 A/B (old = HEAD core.py) with the parity tests first; reused for successive host-side changes
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export C1_WARM=1 C1_EPISODES=20
 bash tools/gpu_round.sh \
