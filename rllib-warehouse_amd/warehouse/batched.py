@@ -44,6 +44,9 @@ def require_device(device=None) -> torch.device:
 def _dev_i32(x, device, shape=None):
     if x is None:
         return None
+    if torch.is_tensor(x) and x.dtype == torch.int32 and x.device == device and x.is_contiguous() \
+            and (shape is None or tuple(x.shape) == tuple(shape)):
+        return x                         # already a device operand: no conversion ops per launch
     t = torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x)
     t = t.to(device=device, dtype=torch.int32).contiguous()
     if shape is not None:
