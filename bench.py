@@ -107,8 +107,9 @@ def cpu_baseline(variant, n, procs, seconds, detail=""):
 
 
 def source_sha():
-    """sha256 of the kernel sources: profile-derived fields are reported only when the committed
-    profile was taken from the same sources."""
+    """sha256 of the kernel sources (csrc/*.hip + *.h, sorted; the hash the Makefile bakes into
+    wh_version()): profile-derived fields are reported only when the committed profile was taken
+    from the same sources, and the run refuses a library built from other sources."""
     import hashlib
 
     h = hashlib.sha256()
@@ -456,6 +457,10 @@ def main():
     dev = torch.device("cuda", local)
 
     import warehouse
+    from warehouse import _native
+
+    # provenance: the loaded library must have been built from this tree's kernel sources
+    binary_sha = _native.verify_provenance()
 
     B, NA, K, W = args.envs, args.agents, args.steps, args.warmup
     env = warehouse.BatchedWarehouse(args.variant, B, NA, seed=1234, env_offset=shard_offset(rank, B), device=dev)
@@ -565,6 +570,8 @@ def main():
                                    "the timed window across an episode end (done + auto-reset + request "
                                    "expiry inside it)"},
             },
+            "binary": {"wh_version": _native.lib().wh_version().decode(), "source_sha": binary_sha,
+                       "tree_source_sha": source_sha(), "path": os.path.relpath(_native.LIB_PATH, ROOT)},
             "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,
             "desync_episodes": desync,

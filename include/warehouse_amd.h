@@ -128,8 +128,8 @@ int wh_observe(const wh_config* cfg, int64_t B, const uint32_t* state, float* ob
  * wh_mlp_forward_x: bf16 in MFMA fragment order, ceil(B*NA/32) tiles of 32 agent rows x KQ =
  * ceil((9R+3)/16) k-steps x 64 lanes x 16 bytes; 16-byte chunk ((tile*KQ + q)*64 + lane) = features
  * 16q + 8(lane>>5) + j, j < 8, of row tile*32 + (lane&31), features 9R+1 and 9R+2 = 1.0, padding 0
- * (rows past B*NA: zero features but the two 1.0 columns).  obs may be NULL.  WH_ENOTSUP for agent counts whose
- * observation workgroups do not hold whole 32-row tiles (e.g. Medium with 9 agents). */
+ * (rows past B*NA: zero features but the two 1.0 columns).  obs may be NULL.  Every agent count
+ * is supported; xfrag must be 16-byte aligned. */
 int wh_observe_x(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* xfrag, void* stream);
 
 #define WH_POLICY_GREEDY 1    /* baseline/solvers.py:27-58 with random_action_prob p */
@@ -169,11 +169,15 @@ int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, 
  * draws, then (autoreset != 0) a philox reset of every env whose episode ended -- Train variants
  * (variable_n != 0) redraw n there, variants.py:69-71 -- then wh_observe into obs (NULL = skip).
  * With autoreset the obs rows of a done env are the first rows of its next episode.
- *   actions [B,NA] int32 0..8 (others act as 4 = stay); mask [B] uint8 or NULL: only envs with
- *   mask != 0 are stepped (the others keep their state; their rewards/dones are not written);
- *   rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats may be NULL. */
+ *   actions [B,NA] int32 0..8 (others act as 4 = stay)
+ *   order   [B,NA] int32 or NULL: each env's action-dict iteration order (core.py:279), -1
+ *           terminated; agents not listed are skipped -- they neither move nor re-mark their cell
+ *           (core.py:279-300 only visits the dict's keys).  NULL = every agent, ascending id.
+ *   mask [B] uint8 or NULL: only envs with mask != 0 are stepped (the others keep their state;
+ *   their rewards/dones are not written); rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats
+ *   may be NULL. */
 int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                   const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
+                   const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream);
 

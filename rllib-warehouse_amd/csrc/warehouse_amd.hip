@@ -1862,14 +1862,6 @@ inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + BT - 1) / BT)); }
 // =============================================================================== C ABI
 extern "C" {
 
-const char* wh_version(void) {
-#ifdef WH_CHECK
-  return "warehouse_amd gfx950 lane-per-env v3 (assert mode) " __DATE__;
-#else
-  return "warehouse_amd gfx950 lane-per-env v3 " __DATE__;
-#endif
-}
-
 int wh_check_read(uint64_t* out, int32_t clear) {
 #ifdef WH_CHECK
   if (!out) return WH_EINVAL;
@@ -2139,9 +2131,16 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   // envs per workgroup: ~40-75 KB of rows per group (measured: 64 for Small-4's 592 B/env rows,
   // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
-  const int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
-  const int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
-  if (xfrag && ((ebx * g.NA) % 32 != 0 || (uintptr_t)xfrag % 16 != 0)) return WH_ENOTSUP;
+  int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
+  int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
+  if (xfrag && (uintptr_t)xfrag % 16 != 0) return WH_EINVAL;
+  // the fragment operand is written in whole 32-row tiles per workgroup: groups of 64 envs hold
+  // 64 * NA rows, a multiple of 32 for every agent count (e.g. Medium with 9 agents, whose f32-row
+  // grouping of 16 envs = 144 rows does not)
+  if (xfrag && (ebx * g.NA) % 32 != 0) {
+    sel = 2;
+    ebx = 64;
+  }
   hipLaunchKernelGGL(k->observe[sel], dim3((unsigned)((B + ebx - 1) / ebx)), dim3(BT), 0,
                      (hipStream_t)stream, state, B, g.NA, tab, obs, quads, static_cast<uint4*>(xfrag));
   return hip_err(hipGetLastError());
@@ -2156,13 +2155,14 @@ int wh_observe_x(const wh_config* cfg, int64_t B, const uint32_t* state, float* 
 }
 
 int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                   const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
+                   const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream) {
   if (B > 0 && !actions) return WH_EINVAL;
   if (!stats_ok(stats)) return WH_EINVAL;
   StepParams a{};
   a.actions = actions;
+  a.order = order;   // non-NULL: the action-dict order path (k_step<..., ORDERED>), as wh_step
   a.mask = mask;
   a.rewards = rewards;
   a.dones = dones;

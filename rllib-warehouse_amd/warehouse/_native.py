@@ -119,7 +119,7 @@ def lib() -> ctypes.CDLL:
     L.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
     _ST = ctypes.POINTER(WhEpisodeStats)
     L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
-    L.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    L.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     _MD = ctypes.POINTER(WhMlpDesc)
     L.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
     L.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
@@ -137,6 +137,53 @@ def lib() -> ctypes.CDLL:
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
+
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def tree_source_sha(csrc: str = CSRC) -> str:
+    """sha256 (16 hex digits) of csrc/*.hip + csrc/*.h in sorted name order: the hash the Makefile
+    bakes into wh_version() and bench.py:source_sha() ties the committed profiles to."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(csrc, f), "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def version_sha(version: bytes) -> Optional[str]:
+    """The source sha a wh_version() string carries ("... sha=<16 hex>"), or None."""
+    v = version.decode(errors="replace")
+    return v.rsplit("sha=", 1)[1].strip() if "sha=" in v else None
+
+
+def file_source_sha(path: str) -> Optional[str]:
+    """The source sha baked into a built library file, read from its bytes (no load)."""
+    import re
+
+    with open(path, "rb") as fh:
+        m = re.search(rb"lane-per-env v3 (?:\(assert mode\) )?sha=([0-9a-f]{16}|unknown)", fh.read())
+    return m.group(1).decode() if m else None
+
+
+def verify_provenance(extra_libs=()) -> str:
+    """Raise WarehouseNativeError unless the loaded library -- and every file in `extra_libs` (e.g.
+    the assert-mode build_ab/check.so) -- was built from the kernel sources in this tree.  Returns
+    the sha."""
+    want = tree_source_sha()
+    got = version_sha(lib().wh_version())
+    if got != want:
+        raise WarehouseNativeError(f"{LIB_PATH} was built from sources sha={got}, the tree has sha={want}: "
+                                   "stale library -- rebuild (__graft_entry__.build())")
+    for p in extra_libs:
+        g = file_source_sha(p) if os.path.exists(p) else "missing"
+        if g != want:
+            raise WarehouseNativeError(f"{p}: built from sources sha={g}, the tree has sha={want}: stale library")
+    return want
 
 
 def check(rc: int, what: str) -> None:

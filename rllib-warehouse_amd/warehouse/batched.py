@@ -221,14 +221,18 @@ class BatchedWarehouse:
                    self._xfrag.data_ptr(), self.stream)
         return (self._xfrag, self._obs) if obs else self._xfrag
 
-    def vector_step(self, actions, autoreset: bool = True, observe: bool = True, mask=None
+    def vector_step(self, actions, autoreset: bool = True, observe: bool = True, mask=None, order=None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
         """Sampler step (wh_vector_step): step every env (or those in the [B] bool `mask`) with
         `actions` [B,NA] (philox draws), restart the envs whose episode ended (autoreset; Train
-        variants redraw n), then write the observation rows.  Returns env-owned (obs [B,NA,9R+1]
-        or None, rewards [B,NA], dones [B]); with autoreset the obs rows of a done env already
-        belong to its next episode.  Rewards/dones of envs outside `mask` are stale."""
+        variants redraw n), then write the observation rows.  `order` [B,NA] (-1 terminated) is
+        each env's action-dict iteration order; agents it does not list are skipped like agents
+        absent from the reference's action dict (core.py:279-300); None = all, ascending.
+        Returns env-owned (obs [B,NA,9R+1] or None, rewards [B,NA], dones [B]); with autoreset the
+        obs rows of a done env already belong to its next episode.  Rewards/dones of envs outside
+        `mask` are stale."""
         a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
+        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
         m = None
         if mask is not None:
             m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
@@ -236,7 +240,7 @@ class BatchedWarehouse:
             self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
                                     device=self.device)
         obs = self._obs if observe else None
-        self._call("wh_vector_step", self.state.data_ptr(), a.data_ptr(), nat.ptr(m), self.rewards.data_ptr(),
+        self._call("wh_vector_step", self.state.data_ptr(), a.data_ptr(), nat.ptr(o), nat.ptr(m), self.rewards.data_ptr(),
                    self.dones.data_ptr(), nat.ptr(obs), None if self.stats is None else self.stats.ref,
                    int(bool(autoreset)), int(self.train), self.seed, self.env_offset, self.stream)
         return obs, self.rewards, self.dones
@@ -311,7 +315,12 @@ class BatchedWarehouse:
                 rc = run(h, e0, e1)
                 if rc:
                     nat.check(rc, "wh_launch_run_timed")
-        launch.keep = (rewards, dones, returns, self.stats, events)   # buffers the handle points into
+        # everything the handle points into: the output buffers and the state tensor (held through
+        # the env; reassigning env.state while the launcher lives is not supported -- the handle
+        # keeps the old tensor alive and writes it).  The launch stream is the one current at
+        # prepare time, for every launch of the handle.
+        launch.keep = (rewards, dones, returns, self.stats, events, self.state, self)
+        launch.stream = self.stream
         weakref.finalize(launch, lib.wh_launch_free, h)
         return launch
 

@@ -79,29 +79,38 @@ class Warehouse(MultiAgentEnv):
         })
 
         self._pickup_set = set(pickup_cells(D, self._pickup_racks_arrangement))
-        geo = dict(D=D, R=R, racks=tuple(self._pickup_racks_arrangement), T=self._episode_duration,
-                   W=self._pickup_wait_duration, max_agents=self._num_agents)
-        self._engine = BatchedWarehouse(num_envs=1, num_agents=self._num_agents, geometry=geo,
-                                        device=_default_device())
         w = {k: n for k, n in zip(OBS_KEYS, (1, R - 1, 2 * (R - 1), 2 * (R - 1), 4 * R, 1, 2, 2))}
         ends = np.cumsum([w[k] for k in OBS_KEYS])
         self._obs_slices = [slice(int(a), int(b)) for a, b in zip(np.r_[0, ends[:-1]], ends)]
         self._done = False
         self._prev = None          # host snapshot before the last step (core.py:270-272), kept
         self._rendering = False    # only once render() has been called: it costs a device copy
-        self._io = None            # per-step upload buffers, sized by num_agents (Train re-inits)
+        # The device engine and its buffers, per configuration.  The Train variants re-run
+        # __init__ at every reset with a new agent count (variants.py:69-71); the engine, its
+        # result block and the pinned upload buffers of an agent count are built once per env object
+        # and reused by every later episode with that count (pinning host memory is slow).
+        geo = dict(D=D, R=R, racks=tuple(self._pickup_racks_arrangement), T=self._episode_duration,
+                   W=self._pickup_wait_duration, max_agents=self._num_agents)
+        cache = self.__dict__.setdefault("_engine_cache", {})
+        key = (self._num_agents, D, R, geo["racks"], geo["T"], geo["W"])
+        if key not in cache:
+            cache[key] = self._build_engine(geo)
+        self._engine, self._blob, self._r_off, self._d_off, io = cache[key]
+        self._io = io              # per-step upload buffers (pinned), created at the first step
+
+    def _build_engine(self, geo):
+        eng = BatchedWarehouse(num_envs=1, num_agents=self._num_agents, geometry=geo, device=_default_device())
         # The engine's observation, reward and done buffers as views of ONE device block, so a step's
         # results come back in a single download with no gather kernel (offsets 256-aligned: the
         # kernels store rows with 16-byte writes).
-        eng = self._engine
         o_bytes = 4 * self._num_agents * eng.obs_len
-        self._r_off = -(-o_bytes // 256) * 256
-        self._d_off = self._r_off + 256 * (-(-4 * self._num_agents // 256))
-        blob = torch.zeros(self._d_off + 256, dtype=torch.uint8, device=eng.device)
+        r_off = -(-o_bytes // 256) * 256
+        d_off = r_off + 256 * (-(-4 * self._num_agents // 256))
+        blob = torch.zeros(d_off + 256, dtype=torch.uint8, device=eng.device)
         eng._obs = blob[:o_bytes].view(torch.float32).view(1, self._num_agents, eng.obs_len)
-        eng.rewards = blob[self._r_off:self._r_off + 4 * self._num_agents].view(torch.float32).view(1, self._num_agents)
-        eng.dones = blob[self._d_off:self._d_off + 1]
-        self._blob = blob
+        eng.rewards = blob[r_off:r_off + 4 * self._num_agents].view(torch.float32).view(1, self._num_agents)
+        eng.dones = blob[d_off:d_off + 1]
+        return [eng, blob, r_off, d_off, None]
 
     # ------------------------------------------------------------------ helpers
     def _io_buffers(self):
@@ -111,6 +120,9 @@ class Warehouse(MultiAgentEnv):
             h_io = torch.empty((2, n), dtype=torch.int32).pin_memory()
             h_regen = torch.empty((1, 2 * R), dtype=torch.int32).pin_memory()
             self._io = (h_io, torch.empty_like(h_io, device=dev), h_regen, torch.empty_like(h_regen, device=dev))
+            for entry in self._engine_cache.values():   # kept with the engine for later episodes
+                if entry[0] is self._engine:
+                    entry[4] = self._io
         return self._io
 
     def _obs_dicts(self, rows: Optional[np.ndarray] = None) -> Dict[str, Dict[str, np.ndarray]]:

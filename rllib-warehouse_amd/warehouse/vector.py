@@ -105,11 +105,13 @@ class WarehouseVectorEnv:
         self.env.reset(mask=mask)
         return self.env.observe()
 
-    def vector_step(self, actions, mask=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, dict]:
+    def vector_step(self, actions, mask=None, order=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, dict]:
         """actions [B,NA] int in 0..8 (values outside act as 4 = stay); `mask` [B] bool limits the
-        step to some envs.  Returns env-owned (obs [B,NA,9R+1], rewards [B,NA], dones [B] bool,
-        infos)."""
-        obs, rew, done = self.env.vector_step(actions, autoreset=self.autoreset, mask=mask)
+        step to some envs; `order` [B,NA] int (-1 terminated) is each env's action-dict order --
+        agents it leaves out are skipped as in the reference (core.py:279-300), None = every agent
+        in ascending id order.  Returns env-owned (obs [B,NA,9R+1], rewards [B,NA], dones [B]
+        bool, infos)."""
+        obs, rew, done = self.env.vector_step(actions, autoreset=self.autoreset, mask=mask, order=order)
         return obs, rew, done.bool(), {}
 
     def agent_mask(self) -> torch.Tensor:
@@ -131,6 +133,7 @@ class WarehouseBaseEnv:
         self.num_envs = self.vec.num_envs
         self.observation_space = self.vec.observation_space
         self.action_space = self.vec.action_space
+        self._n = np.zeros(self.num_envs, np.int64)   # agents of each env's episode (host copy)
         obs = self.vec.vector_reset()
         self._pending = self._pack(obs, None, None, range(self.num_envs))
 
@@ -160,6 +163,7 @@ class WarehouseBaseEnv:
         agent_ids = [str(i) for i in range(NA)]
         rl = None if r is None else r.tolist()
         dl = [False] * len(env_ids) if d is None else d.tolist()
+        self._n[env_ids] = n
         res = ({}, {}, {}, {}, {})
         for k, e in enumerate(env_ids):
             nk = int(n[k])
@@ -180,18 +184,35 @@ class WarehouseBaseEnv:
         return out
 
     def send_actions(self, action_dict: Dict[int, Dict[str, int]]) -> None:
-        """Step the envs named in `action_dict` (other envs are untouched; an agent missing from
-        its env's dict takes action 4 = stay).  Actions wrap like Python indexing (core.py:279-281)."""
-        acts = np.full((self.num_envs, self.vec.num_agents), 4, np.int32)
+        """Step the envs named in `action_dict` (other envs are untouched) with the reference's
+        dict semantics (core.py:279-300): each env's agents are resolved in its dict's iteration
+        order, and an agent missing from the dict is skipped -- it neither moves nor re-marks its
+        cell (a "stay" would), so a later agent may enter a cell a co-located agent just left.
+        Actions wrap like Python indexing; >= 9 raises IndexError (MOVES[action], core.py:281),
+        and so does an agent id outside the env's episode (agent_positions[idx], core.py:280)."""
+        NA = self.vec.num_agents
+        acts = np.full((self.num_envs, NA), 4, np.int32)
+        order = np.full((self.num_envs, NA), -1, np.int32)
         mask = np.zeros(self.num_envs, bool)
+        ascending = True            # every dict lists all agents of its env in ascending order
         for e, ad in action_dict.items():
             mask[e] = True
-            for a, v in ad.items():
-                v = int(v)
+            n = int(self._n[e])
+            if len(ad) > NA:
+                raise ValueError(f"env {e}: {len(ad)} actions for {NA} agent slots")
+            for s, (a, v) in enumerate(ad.items()):
+                idx, v = int(a), int(v)
                 if not -9 <= v < 9:
                     raise IndexError("list index out of range")   # MOVES[a], core.py:281
-                acts[e, int(a)] = v % 9
-        obs, rew, done, _ = self.vec.vector_step(acts, mask=mask)
+                if not 0 <= idx < n:
+                    raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
+                acts[e, idx] = v % 9
+                order[e, s] = idx
+                ascending = ascending and idx == s
+            ascending = ascending and len(ad) == n
+        # the ascending kernel when every dict is full and in id order (the common sampler case),
+        # else the dict-order kernel
+        obs, rew, done, _ = self.vec.vector_step(acts, mask=mask, order=None if ascending else order)
         self._pending = self._pack(obs, rew, done, sorted(action_dict))
 
     def try_reset(self, env_id: int) -> Dict[str, np.ndarray]:

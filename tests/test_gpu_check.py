@@ -29,6 +29,7 @@ import warehouse
 from warehouse import _native as nat
 lib = nat.lib()
 assert b"assert mode" in lib.wh_version(), lib.wh_version()
+assert nat.version_sha(lib.wh_version()) == nat.tree_source_sha(), "stale check.so"
 out = (ctypes.c_uint64 * 4)()
 def read(clear=1):
     assert lib.wh_check_read(out, clear) == 0

@@ -471,14 +471,18 @@ def test_timed_launch_equals_rollout_and_stamps_events(wh):
     assert spans[60] > spans[5]
 
 
-@pytest.mark.parametrize("variant,na", [("medium", 8), ("large", 16)])
-def test_fast_rollout_co_located_agents_vs_oracle(wh, variant, na):
-    """The fast fused instance (rewards + dones, auto-reset) on states where agents share cells.
-    A co-located agent leaving clears the cell under the one that stays (core.py:289-291) until
-    the next step's rebuild (core.py:275-276); the fast instance rebuilds only for lanes whose
-    co-located agents moved, so this is its exactness case: up to half the agents start in pairs
-    on shared cells (pairs that stay put keep sharing), and the rollout crosses two episode ends
-    (fresh spawns share cells again)."""
+@pytest.mark.parametrize("variant,na,policy,p", [("medium", 8, "greedy", 0.0), ("large", 16, "greedy", 0.0),
+                                                  ("medium", 8, "greedy", 0.25), ("large", 16, "greedy", 0.1),
+                                                  ("medium", 8, "random", 0.0), ("small", 4, "random", 0.0)])
+def test_fast_rollout_co_located_agents_vs_oracle(wh, variant, na, policy, p):
+    """The fast fused instance (rewards + dones only, auto-reset: lazy occupancy grid, unclamped
+    greedy steps, random moves converted to the steps they take) on states where agents share
+    cells.  A co-located agent leaving clears the cell under the one that stays (core.py:289-291)
+    until the next step's rebuild (core.py:275-276); the fast instance rebuilds only for lanes
+    whose co-located agents moved, so this is its exactness case: up to half the agents start in
+    pairs on shared cells (pairs that stay put keep sharing), and the rollout crosses two episode
+    ends (fresh spawns share cells again).  Greedy with p > 0 and the random policy put random
+    moves (including off-grid ones, core.py:282-287) through the same path."""
     import torch
 
     B, seed, K = 2048, 17, 430
@@ -498,12 +502,43 @@ def test_fast_rollout_co_located_agents_vs_oracle(wh, variant, na):
     S = oracle_state(canon(env), L)
     rew = torch.zeros((K, B, na), device=env.device)
     dn = torch.zeros((K, B), dtype=torch.uint8, device=env.device)
-    env.rollout(K, "greedy", 0.0, rewards=rew, dones=dn)
+    env.rollout(K, policy, p, rewards=rew, dones=dn)          # no returns/stats: the fast instance
     d = ob.PhiloxDraws(seed, np.arange(B))
     for s in range(K):
-        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        acts = ob.greedy(L, S, p, d) if policy == "greedy" else ob.random_actions(S, d)
+        orew, odone, _, _ = ob.step(L, S, acts, d)
         np.testing.assert_array_equal(rew[s].cpu().numpy(), orew, err_msg=f"step {s}")
         np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
         if odone.any():
             ob.reset(L, S, d, mask=odone)
     assert_same(canon(env), S, "after rollout")
+
+
+@pytest.mark.parametrize("variant,na", [("medium", 5), ("large", 7)])
+def test_ordered_path_na_below_kernel_slots_vs_oracle(wh, variant, na):
+    """The action-dict-order kernel (wh_step with `order`) at B = 2048 with fewer agents than the
+    kernel's compile-time slots (Medium-5 runs the 8-slot instance, Large-7 the 8-slot one): the
+    odd-NA reward rows are staged in LDS inside each wave's own columns (the path that carried
+    round 2's cross-wave race), shuffled and partial dicts, philox regeneration; 120 steps across
+    t = T (no auto-reset in wh_step) vs the oracle."""
+    B, seed, K = 2048, 23, 205
+    L = oc.layout_for(variant)
+    env = wh.BatchedWarehouse(variant, B, na, seed=seed)
+    env.reset()
+    S = ob.BState.zeros(L, B, na)
+    d = ob.PhiloxDraws(seed, np.arange(B))
+    ob.reset(L, S, d, n_fixed=na)
+    rng = np.random.RandomState(8)
+    for s in range(K):
+        acts = rng.randint(0, 9, size=(B, na)).astype(np.int32)
+        order = np.full((B, na), -1, np.int32)
+        for e in range(B):
+            k = na if rng.rand() < 0.4 else rng.randint(0, na + 1)
+            order[e, :k] = rng.permutation(na)[:k]
+        rew, done = env.step(acts, order=order)
+        orew, odone, _, _ = ob.step(L, S, acts, d, order=order)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
+        if s % 20 == 0 or s >= 195:
+            assert_same(canon(env), S, f"step {s}")
+    np.testing.assert_array_equal(env.observe().cpu().numpy(), ob.observe(L, S))

@@ -117,24 +117,30 @@ def test_mlp_edge_cases(wh):
                                     None, 0, 0, 0, None) == nat.WH_ENOTSUP
 
 
-@pytest.mark.parametrize("operand", ["fragments", "rows"])
-def test_policy_rollout_transitions_vs_oracle(wh, operand):
+@pytest.mark.parametrize("variant,na,train,operand", [("medium", 8, False, "fragments"), ("medium", 8, False, "rows"),
+                                                       ("medium", 9, False, "auto"), ("medium", None, True, "auto"),
+                                                       ("large", 5, False, "auto"), ("small", None, True, "auto")])
+def test_policy_rollout_transitions_vs_oracle(wh, variant, na, train, operand):
     """The device policy loop (network forward -> wh_vector_step with auto-reset) for 230 steps, on
     the fragment-order operand and on the f32 rows: actions equal a separate forward on the same
-    rows, and every transition equals the oracle's given those actions (philox draws)."""
+    rows, and every transition equals the oracle's given those actions (philox draws).  Includes
+    the default BatchedWarehouse('medium', B) (9 agent slots), the Train variants (per-episode n)
+    and agent counts whose observation workgroups do not hold whole 32-row fragment tiles."""
     import torch
 
     from oracle import batched as ob
     from oracle import core as oc
 
-    B, na, seed = 512, 8, 17
-    L = oc.layout_for("medium")
-    env = wh.BatchedWarehouse("medium", B, na, seed=seed)
+    B, seed = 512, 17
+    L = oc.layout_for(variant)
+    env = wh.BatchedWarehouse(variant, B, na, train=train, seed=seed)
+    na = env.agent_slots
     env.reset()
-    net = wh.policy.MLPPolicy("medium", seed=2)
+    net = wh.policy.MLPPolicy(variant, seed=2)
     S = ob.BState.zeros(L, B, na)
     d = ob.PhiloxDraws(seed, np.arange(B))
-    ob.reset(L, S, d)
+    nmax = na if train else None
+    ob.reset(L, S, d, nmax=nmax)
     log = []
 
     def record(s, acts, rew, done):
@@ -149,7 +155,7 @@ def test_policy_rollout_transitions_vs_oracle(wh, operand):
         np.testing.assert_array_equal(rew, orew, err_msg=f"step {s}")
         np.testing.assert_array_equal(done.astype(bool), odone)
         if odone.any():
-            ob.reset(L, S, d, mask=odone)
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
     np.testing.assert_array_equal(env.observe().cpu().numpy(), ob.observe(L, S))
     assert len({int(x) for x in np.unique(np.concatenate([a.reshape(-1) for a, _, _ in log]))}) > 1
 
@@ -213,7 +219,8 @@ def frag_reference(rows_f32, kq):
     return out
 
 
-@pytest.mark.parametrize("variant,na,B", [("small", 4, 100), ("medium", 8, 61), ("large", 16, 37)])
+@pytest.mark.parametrize("variant,na,B", [("small", 4, 100), ("medium", 8, 61), ("large", 16, 37),
+                                          ("medium", 9, 150), ("large", 5, 70), ("small", 3, 131)])
 def test_observe_x_fragments_and_forward_x(wh, variant, na, B):
     """wh_observe_x writes exactly the bf16 fragment image of wh_observe's rows (bias columns 1.0,
     padding 0, ragged last tile), and wh_mlp_forward_x on it gives bit-identical logits and actions

@@ -181,9 +181,13 @@ def test_base_env_poll_send_try_reset(wh):
         be.send_actions({0: {"0": 9}})
 
 
-@pytest.mark.parametrize("variant,na,train", [("medium", 8, False), ("large", 16, False), ("large", 16, True),
-                                              ("small", 4, True)])
-def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na, train):
+@pytest.mark.parametrize("variant,na,train,policy,p", [("medium", 8, False, "greedy", 0.0),
+                                                        ("large", 16, False, "greedy", 0.0),
+                                                        ("large", 16, True, "greedy", 0.0),
+                                                        ("small", 4, True, "greedy", 0.0),
+                                                        ("medium", 8, False, "greedy", 0.2),
+                                                        ("medium", 8, False, "random", 0.0)])
+def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na, train, policy, p):
     """Desynchronised episodes (BatchedWarehouse.stagger: env e takes e*7 % 200 extra masked greedy
     steps), then a 260-step fused rollout: every step some envs end, reset and run the expiry pass
     while their wave-mates do not (one env per wave: the wave-wide single-env reset and expiry).
@@ -212,11 +216,12 @@ def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na, train):
     assert len(np.unique(S.t)) > 150                       # episode clocks are spread out
     rew = torch.zeros((K, B, na), device=env.device)
     dn = torch.zeros((K, B), dtype=torch.uint8, device=env.device)
-    env.rollout(K, "greedy", 0.0, rewards=rew, dones=dn)
+    env.rollout(K, policy, p, rewards=rew, dones=dn)
     d = ob.PhiloxDraws(seed, ids)
     ends = 0
     for s in range(K):
-        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        acts = ob.greedy(L, S, p, d) if policy == "greedy" else ob.random_actions(S, d)
+        orew, odone, _, _ = ob.step(L, S, acts, d)
         np.testing.assert_array_equal(rew[s].cpu().numpy(), orew, err_msg=f"step {s}")
         np.testing.assert_array_equal(dn[s].cpu().numpy().astype(bool), odone, err_msg=f"step {s}")
         ends += int(odone.sum())
@@ -228,3 +233,163 @@ def test_staggered_episodes_fused_rollout_vs_oracle(wh, variant, na, train):
     np.testing.assert_array_equal(c["pickup_target"], S.pk_tgt)
     np.testing.assert_array_equal(c["t"], S.t)
     np.testing.assert_array_equal(c["n"], S.n)
+
+
+# ----------------------------------------------------------------------------- action-dict order
+def fixture_pre_states(g):
+    """The fixture's state before each of its 200 steps (reset state, then the state after step
+    s-1) as canonical arrays [200, ...]."""
+    n = int(g["n"])
+    pos = np.concatenate([g["reset_pos"][None], g["pos"][:-1]])
+    atg = np.concatenate([g["reset_agent_tgt"][None], g["agent_tgt"][:-1]])
+    ptg = np.concatenate([g["reset_pk_tgt"][None], g["pk_tgt"][:-1]])
+    ptm = np.concatenate([g["reset_pk_timer"][None], g["pk_timer"][:-1]])
+    t = np.concatenate([[int(g["reset_t"])], g["t"][:-1]]).astype(np.int32)
+    return dict(pos=pos, agent_target=atg, pickup_target=ptg, pickup_timer=ptm, t=t,
+                n=np.full(len(t), n, np.int32))
+
+
+@pytest.mark.parametrize("variant", ["small", "medium", "large"])
+def test_base_env_replays_reference_dict_order_fixtures(wh, variant):
+    """tests/golden/ord_*: the reference's own episodes driven by shuffled and partial action dicts
+    with negative actions (core.py:279-300), replayed through WarehouseBaseEnv.send_actions as one
+    batch -- env s holds the reference's state before step s and gets that step's dict, in two
+    masked halves (odd envs first).  Everything the regeneration draws do not touch equals the
+    reference bit for bit (positions, carried targets, rewards, dones, every request not reopened
+    this step, the count reopened); the whole transition including the philox regeneration and
+    the observation rows equals the oracle's."""
+    from warehouse.vector import WarehouseBaseEnv
+
+    L = oc.layout_for(variant)
+    import glob
+    import os
+
+    paths = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", f"ord_{variant}_*.npz")))
+    assert paths
+    for path in paths:
+        g = np.load(path)
+        n = int(g["n"])
+        steps = len(g["t"])
+        pre = fixture_pre_states(g)
+        be = WarehouseBaseEnv(variant, steps, n, train=False, seed=9)
+        be.vec.env.from_canonical(pre)
+        be._n[:] = n
+        dicts = {s: {str(int(i)): int(g["actions"][s][int(i)]) for i in g["order"][s] if i >= 0}
+                 for s in range(steps)}
+        assert any(len(d) < n for d in dicts.values()) and any(list(d) != sorted(d, key=int) for d in dicts.values())
+        got_rew, got_done = {}, {}
+        for half in (1, 0):
+            be.send_actions({s: dicts[s] for s in range(steps) if s % 2 == half})
+            _, rew, dones, _, _ = be.poll()
+            assert sorted(rew) == [s for s in range(steps) if s % 2 == half]
+            got_rew.update(rew)
+            got_done.update(dones)
+        c = {k: v.cpu().numpy() for k, v in be.vec.env.to_canonical().items()}
+        W = L.W
+        for s in range(steps):
+            msg = f"{path} step {s}"
+            np.testing.assert_array_equal(c["pos"][s], g["pos"][s], err_msg=msg)
+            np.testing.assert_array_equal(c["agent_target"][s], g["agent_tgt"][s], err_msg=msg)
+            assert [got_rew[s][str(i)] for i in range(n)] == list(g["rewards"][s]), msg
+            assert got_done[s]["__all__"] == bool(g["done"][s]), msg
+            ro, rf = c["pickup_timer"][s] == W, g["pk_timer"][s] == W       # reopened this step
+            assert ro.sum() == rf.sum(), msg
+            keep = ~(ro | rf)
+            np.testing.assert_array_equal(c["pickup_target"][s][keep], g["pk_tgt"][s][keep], err_msg=msg)
+            np.testing.assert_array_equal(c["pickup_timer"][s][keep], g["pk_timer"][s][keep], err_msg=msg)
+            assert (c["pickup_target"][s][rf & ~ro] == -1).all() and (g["pk_tgt"][s][ro & ~rf] == -1).all()
+        # the whole transition, philox regeneration included, against the oracle
+        S = ob.BState(pos=pre["pos"].copy(), agent_tgt=pre["agent_target"].copy(),
+                      pk_tgt=pre["pickup_target"].copy(), pk_timer=pre["pickup_timer"].copy(),
+                      t=pre["t"].astype(np.int64), n=pre["n"].copy(), fresh=np.zeros(steps, bool),
+                      episode=np.zeros(steps, np.uint32))
+        acts = np.full((steps, n), 4, np.int32)
+        order = np.full((steps, n), -1, np.int32)
+        for s, d in dicts.items():
+            for k, (a, v) in enumerate(d.items()):
+                acts[s, int(a)] = v % 9
+                order[s, k] = int(a)
+        orew, odone, _, _ = ob.step(L, S, acts, ob.PhiloxDraws(9, np.arange(steps)), order=order)
+        np.testing.assert_array_equal(np.array([[got_rew[s][str(i)] for i in range(n)] for s in range(steps)]), orew)
+        for f, k in (("pos", "pos"), ("agent_target", "agent_tgt"), ("pickup_target", "pk_tgt"),
+                     ("pickup_timer", "pk_timer"), ("t", "t")):
+            np.testing.assert_array_equal(c[f], getattr(S, k), err_msg=f)
+        np.testing.assert_array_equal(be.vec.env.observe().cpu().numpy(), ob.observe(L, S))
+
+
+def test_base_env_absent_agent_does_not_remark_its_cell(wh):
+    """Known-answer test of core.py:279-300's dict semantics on co-located agents (Small, 3
+    agents; 0 and 1 share cell (2,2), agent 2 at (3,2); action 1 = move -x):
+      env 0  {"0": 1, "2": 1}          agent 0 leaves (clearing the shared cell), agent 1 is absent
+                                       and does not re-mark it, so agent 2 enters: 1 and 2 share it
+      env 1  {"0": 1, "1": 4, "2": 1}  agent 1's "stay" re-marks the cell: agent 2 is blocked
+      env 2  {"2": 1, "0": 1}          agent 2 goes first and is blocked, then agent 0 leaves
+      env 3  {}                        nobody moves
+    and the same through the oracle for every env."""
+    from warehouse.vector import WarehouseBaseEnv
+
+    L = oc.layout_for("small")
+    B, n = 4, 3
+    pos = np.tile(np.array([[2, 2], [2, 2], [3, 2]], np.int32), (B, 1, 1))
+    ptg = np.full((B, L.P), -1, np.int32)
+    ptm = np.full((B, L.P), -1, np.int32)
+    ptg[:, :L.R] = np.arange(L.R)
+    ptm[:, :L.R] = 150
+    state = dict(pos=pos, agent_target=np.full((B, n), -1, np.int32), pickup_target=ptg, pickup_timer=ptm,
+                 t=np.full(B, 10, np.int32), n=np.full(B, n, np.int32))
+    be = WarehouseBaseEnv("small", B, n, train=False, seed=4)
+    be.vec.env.from_canonical(state)
+    be._n[:] = n
+    dicts = {0: {"0": 1, "2": 1}, 1: {"0": 1, "1": 4, "2": 1}, 2: {"2": 1, "0": 1}, 3: {}}
+    be.send_actions(dicts)
+    be.poll()
+    got = be.vec.env.to_canonical()["pos"].cpu().numpy()
+    np.testing.assert_array_equal(got[0], [[1, 2], [2, 2], [2, 2]])
+    np.testing.assert_array_equal(got[1], [[1, 2], [2, 2], [3, 2]])
+    np.testing.assert_array_equal(got[2], [[1, 2], [2, 2], [3, 2]])
+    np.testing.assert_array_equal(got[3], [[2, 2], [2, 2], [3, 2]])
+    S = ob.BState(pos=pos.copy(), agent_tgt=state["agent_target"].copy(), pk_tgt=ptg.copy(), pk_timer=ptm.copy(),
+                  t=state["t"].astype(np.int64), n=state["n"].copy(), fresh=np.zeros(B, bool),
+                  episode=np.zeros(B, np.uint32))
+    acts = np.full((B, n), 4, np.int32)
+    order = np.full((B, n), -1, np.int32)
+    for e, d in dicts.items():
+        for k, (a, v) in enumerate(d.items()):
+            acts[e, int(a)] = v
+            order[e, k] = int(a)
+    ob.step(L, S, acts, ob.PhiloxDraws(4, np.arange(B)), order=order)
+    np.testing.assert_array_equal(got, S.pos)
+    with pytest.raises(IndexError):
+        be.send_actions({0: {"3": 4}})                    # no agent 3 in a 3-agent episode
+
+
+@pytest.mark.parametrize("variant,na,train", [("medium", 9, True), ("large", 16, False), ("small", 4, False)])
+def test_vector_step_dict_order_masked_autoreset_vs_oracle(wh, variant, na, train):
+    """wh_vector_step with an action-dict order per env (random permutations of random subsets of
+    the live agents: shuffled and partial dicts), env masks and auto-reset, 230 steps: rewards,
+    dones and observation rows equal the oracle's every step."""
+    B, seed, K = 1024, 29, 230
+    L = oc.layout_for(variant)
+    venv = wh.vector.WarehouseVectorEnv(variant, B, na, train=train, seed=seed)
+    venv.vector_reset()
+    S = ob.BState.zeros(L, B, na)
+    ob.reset(L, S, ob.PhiloxDraws(seed, np.arange(B)), nmax=na if train else None)
+    rng = np.random.RandomState(3)
+    for s in range(K):
+        acts = rng.randint(0, 9, size=(B, na)).astype(np.int32)
+        order = np.full((B, na), -1, np.int32)
+        for e in range(B):
+            k = int(S.n[e]) if rng.rand() < 0.3 else rng.randint(0, int(S.n[e]) + 1)
+            order[e, :k] = rng.permutation(int(S.n[e]))[:k]
+        m = np.ones(B, bool) if s % 5 else rng.rand(B) < 0.6
+        obs, rew, done, _ = venv.vector_step(acts, mask=None if m.all() else m, order=order)
+        idx = np.flatnonzero(m)
+        sub = take(S, idx)
+        d = ob.PhiloxDraws(seed, idx)
+        orew, odone, _, _ = ob.step(L, sub, acts[idx], d, order=order[idx])
+        np.testing.assert_array_equal(rew.cpu().numpy()[idx], orew, err_msg=f"step {s}")
+        np.testing.assert_array_equal(done.cpu().numpy()[idx], odone, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, sub, d, mask=odone, nmax=na if train else None)
+        put(S, idx, sub)
+        np.testing.assert_array_equal(obs.cpu().numpy(), ob.observe(L, S), err_msg=f"obs step {s}")

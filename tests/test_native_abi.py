@@ -34,6 +34,17 @@ def test_library_exports_every_declared_symbol():
     assert _native.lib().wh_version().startswith(b"warehouse_amd gfx950")
 
 
+def test_library_built_from_this_tree():
+    """Provenance: wh_version() carries the sha of the kernel sources the library was built from
+    (Makefile), equal to the tree's; the assert-mode build carries the same sha."""
+    from warehouse import _native
+
+    sha = _native.tree_source_sha()
+    assert _native.version_sha(_native.lib().wh_version()) == sha
+    assert _native.verify_provenance(extra_libs=[os.path.join(ROOT, "build_ab", "check.so")]) == sha
+    assert _native.file_source_sha(_native.LIB_PATH) == sha
+
+
 @pytest.mark.parametrize("variant", ["small", "medium", "large"])
 def test_query_layouts(variant):
     from warehouse import _native
