@@ -298,14 +298,16 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist, position=True):
 
 def measure_sampler(env, K, W, dev, world, dist):
     """The RLlib sampler route (scripts/train.py's workload): per step the device greedy policy
-    stands in for the learner's policy, then wh_vector_step = step + auto-reset + observation
-    rows [B,NA,9R+1] f32.  hipGraph of G steps.  Returns (elapsed_s, observe_kernel_ms)."""
+    stands in for the learner's policy -- fused into the step launch (BatchedWarehouse.sampler_step:
+    one 1-step wh_rollout = policy + step + auto-reset, then wh_observe = observation rows
+    [B,NA,9R+1] f32).  hipGraph of G steps.  Returns (elapsed_s, {kernel: ms per launch}) with each
+    kernel timed alone between HIP events on the launch stream (20 back-to-back launches)."""
     import torch
 
     stream = torch.cuda.current_stream(dev)
 
     def one():
-        env.vector_step(env.policy("greedy", 0.0), autoreset=True, observe=True)
+        env.sampler_step("greedy", 0.0, observe=True)
 
     for _ in range(max(W, 3)):
         one()
@@ -324,16 +326,22 @@ def measure_sampler(env, K, W, dev, world, dist):
             one()
 
     elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
-    # observe kernel alone: 20 back-to-back launches between HIP events on the launch stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
-    for a, b in evs:
-        a.record(stream)
-        for _ in range(20):
-            env.observe()
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    kms = sorted(a.elapsed_time(b) / 20 for a, b in evs)
-    return elapsed, kms[len(kms) // 2]
+
+    def per_launch(fn):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for a, b in evs:
+            a.record(stream)
+            for _ in range(20):
+                fn()
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        kms = sorted(a.elapsed_time(b) / 20 for a, b in evs)
+        return kms[len(kms) // 2]
+
+    split = {"k_observe": per_launch(env.observe),
+             "k_step (1-step rollout: greedy + step + auto-reset)": per_launch(
+                 lambda: env.sampler_step("greedy", 0.0, observe=False))}
+    return elapsed, split
 
 
 def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
@@ -502,13 +510,16 @@ def main():
     sampler = None
     if not args.no_sampler:
         Ks = min(K, 1000)
-        el3, oms = measure_sampler(env, Ks, W, dev, world, dist)
+        el3, split = measure_sampler(env, Ks, W, dev, world, dist)
+        oms = split["k_observe"]
         obs_b = B * NA * env.obs_len * 4 + B * 4 * words     # rows written + packed state read
         sampler = {
-            "workload": f"RLlib sampler route: device greedy actions -> wh_vector_step (step + auto-reset "
-                        f"+ f32 observation rows [B,{NA},{env.obs_len}]), hipGraph of 100 steps",
+            "workload": f"RLlib sampler route: device greedy policy fused with step + auto-reset (one 1-step "
+                        f"wh_rollout launch), then f32 observation rows [B,{NA},{env.obs_len}] (wh_observe); "
+                        f"hipGraph of 100 steps",
             "value": aggregate_rate(world, B, NA, Ks, el3), "unit": "agent-steps/s", "steps": Ks,
             "ms_per_step": el3 * 1e3 / Ks,
+            "kernel_split_ms": dict(split, rest=el3 * 1e3 / Ks - sum(split.values())),
             "roofline": {"bound": "hbm", "kernel": "k_observe", "kernel_ms": oms,
                          "bytes_per_launch": obs_b, "achieved": obs_b / (oms * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

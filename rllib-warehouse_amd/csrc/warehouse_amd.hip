@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 #include <new>
 #include <stdint.h>
 #include <stdlib.h>
@@ -44,6 +45,19 @@ constexpr int PH_ALL = 0, PH_PRE = 1, PH_REGEN = 2, PH_POLICY = 3;
 constexpr bool kAblationBuild = true;    // ablation moves are arbitrary: keep the off-grid clamp
 #else
 constexpr bool kAblationBuild = false;
+#endif
+
+// A/B switches of the fused fast path (tools/anat_ab.sh): -DWH_NO_BIAS keeps plain occupancy-row
+// addressing, -DWH_NO_REGEN_HOIST computes the regeneration's Philox block inside the regeneration.
+#ifndef WH_NO_BIAS
+constexpr bool kBiasAddr = true;
+#else
+constexpr bool kBiasAddr = false;
+#endif
+#ifndef WH_NO_REGEN_HOIST
+constexpr bool kRegenHoist = true;
+#else
+constexpr bool kRegenHoist = false;
 #endif
 
 constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle agent
@@ -648,6 +662,9 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   uint32_t t = s.hdr & 0xFFFFu;
   uint32_t rewm[C::NAM];   // reward masks: all-ones = 1.0f
+  constexpr bool HOIST = LAZY && !INJ && kRegenHoist;   // (see the move phase)
+  uint4 rblk0 = make_uint4(0u, 0u, 0u, 0u);
+  bool hoisted = false;
 
   if (phase != PH_REGEN) {
     t = (t + 1u) & 0xFFFFu;                                 // core.py:267
@@ -714,6 +731,10 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 
     // ---- move + collision, sequential in action-dict order (core.py:275-300)
     WH_PHASE_MARK(move);
+    // The fused rollout's regeneration almost always draws (some lane of the wave reopens a point
+    // on nearly every step), so its first Philox block -- a chain of ten dependent rounds -- is
+    // computed inside the move loop's basic block, where the scheduler fills the serial chain's
+    // issue gaps with it, instead of on its own after the pickups.
     uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329): cell_row,
                                                     // target byte, delivery cell
     bool looked = false;
@@ -810,53 +831,95 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         // agent s updates the grid) and corrected in registers for agent s's clear/set, so no
         // LDS round trip sits on the serial chain; agent s's pickup lookups (cell -> point, point
         // -> target byte, target -> cell) are issued on turns s, s+1, s+2.
+        // BIAS (greedy steps, never off the grid): positions carry the lane id in bits 8-15
+        // (x | lane << 8 | y << 16), so `q >> 6` is the byte offset of the occupancy word
+        // occ[y][lane] (y * 1024 + lane * 4; x < 32) -- one shift per LDS address instead of a
+        // field extract and a shift-or.  Equality tests, x-bit selects and the square key's
+        // packed minimum are unaffected (every position of a lane carries the same lane bits).
+        constexpr bool BIAS = !CLAMP && kBiasAddr;
+        static_assert(BT * 4 == 1024 && C::D <= 32, "occ[y][lane] = byte y << 10 | lane << 2");
+        const uint32_t lbias = BIAS ? ((uint32_t)tid & 255u) << 8 : 0u;
+        auto occ_at = [&](uint32_t q) -> uint32_t* {
+          if constexpr (BIAS)
+            return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(&L.occ[0][0]) + (q >> 6));
+          else
+            return &L.occ[q >> 16][tid];
+        };
         uint32_t pp[C::NAM], cc[C::NAM];
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) {
-          pp[i] = s.ag[i] & XY16;
+          pp[i] = (s.ag[i] & XY16) | lbias;
           cc[i] = CLAMP ? step16<C::D>(pp[i], dstep[i]) : as_u(as_s2(pp[i]) + as_s2(dstep[i]));
         }
         // Predicates are kept in bit 31 of VGPRs (x31 names) and selects are v_bitop3 with
         // 0 / all-ones masks (m names): no VCC round trips on the serial chain.
-        uint32_t raw = L.occ[cc[0] >> 16][tid];
-        uint32_t mokp = 0u;
-#pragma unroll
-        for (int sidx = 0; sidx < C::NAM; ++sidx) {
-          const uint32_t p = pp[sidx], c = cc[sidx], a = s.ag[sidx];
-          // occupied: bit c of the row word, corrected for agent sidx-1's clear-then-set
-          uint32_t occ31 = (uint32_t)__builtin_amdgcn_sbfe((int)raw, c, 1);
-          if (sidx > 0) {
-            const uint32_t set31 = (c ^ cc[sidx - 1]) - 1u;   // bit 31: c == its new cell
-            const uint32_t clr31 = (c ^ pp[sidx - 1]) - 1u;   // bit 31: c == its old cell
-            occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokp, set31, bop3<TC & ~(TA & TB)>(mokp, clr31, occ31));
+        //
+        // Forbidden moves (core.py:293-297): the reverse of every accepted move, matched as an
+        // ordered (from, to) key, and for accepted diagonals the two crossing moves.  A move's
+        // square key is the low corner of the 2x2 square it spans plus dx*dy in the top byte
+        // (0x01 one diagonal, 0xFF the other, 0 straight or stay); "either crossing move of i" is
+        // exactly "same square, opposite diagonal", i.e. square key == i's with the top byte
+        // flipped (^ 0xFE000000: 0x01 <-> 0xFF), which no straight move's key (0) ever equals.
+        // REV = false drops the reverse keys: a later agent can stand on the cell an accepted move
+        // went to only if that cell had been freed by a co-located agent leaving it (the grid was
+        // rebuilt from every position, and a move is accepted only into a free cell), so without
+        // co-located agents in the lane no reverse key can ever match.  The lazy grid knows the
+        // lanes with shared cells (lg->cm, from the last rebuild; new sharing needs an existing
+        // one), so a wave with none of them tests the crossing keys only -- one xor per earlier
+        // agent, reduced three at a time, instead of two xors and a min3.
+        auto move_loop = [&](auto rev_tag) {
+          constexpr bool REV = decltype(rev_tag)::value;
+          if constexpr (HOIST) {   // (an opaque zero keeps LLVM from hoisting it above the branch)
+            uint32_t z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            rblk0 = stream_block(k, gid ^ z, s.epi, t, PUR_REGEN, 0u);
+            hoisted = true;
           }
-          if (sidx + 1 < C::NAM) raw = L.occ[cc[sidx + 1] >> 16][tid];   // before this turn's update
-          // forbidden moves (core.py:293-297): the reverse of every accepted move, matched as an
-          // ordered (from, to) key, and for accepted diagonals the two crossing moves.  A move's
-          // square key is the low corner of the 2x2 square it spans plus dx*dy in the top byte
-          // (0x01 one diagonal, 0xFF the other, 0 straight or stay); "either crossing move of i" is
-          // exactly "same square, opposite diagonal", i.e. square key == i's with the top byte
-          // flipped (^ 0xFE000000: 0x01 <-> 0xFF), which no straight move's key (0) ever equals.
-          const uint32_t key = p | (c << 8);
-          const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
-          const uint32_t ukey = pk_min_u16(p, c) + (mul_swap(dd) << 24);   // top byte dx*dy: 1, 0xFF, 0
-          uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor stays above this
+          uint32_t raw = *occ_at(cc[0]);
+          uint32_t mokp = 0u;
 #pragma unroll
-          for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
-          const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
-          const uint32_t mok = sgn(bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u));
-          atomicAnd(&L.occ[p >> 16][tid], bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
-          atomicOr(&L.occ[c >> 16][tid], bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
-          const uint32_t dxy = c ^ p;
-          rk[sidx] = bop3<~TA | TB>(mok, c | (p << 8), 0u);
-          xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
-          const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
-          s.ag[sidx] = moved;
-          mokp = mok;
-          cp[sidx] = L.cell_row(moved);
-          if (sidx >= 1) tb[sidx - 1] = *L.row_byte(cp[sidx - 1], tid);
-          if (sidx >= 2) dst[sidx - 2] = L.dst_tb(tb[sidx - 2]);
-        }
+          for (int sidx = 0; sidx < C::NAM; ++sidx) {
+            const uint32_t p = pp[sidx], c = cc[sidx], a = s.ag[sidx];
+            // occupied: bit c of the row word, corrected for agent sidx-1's clear-then-set
+            uint32_t occ31 = (uint32_t)__builtin_amdgcn_sbfe((int)raw, c, 1);
+            if (sidx > 0) {
+              const uint32_t set31 = (c ^ cc[sidx - 1]) - 1u;   // bit 31: c == its new cell
+              const uint32_t clr31 = (c ^ pp[sidx - 1]) - 1u;   // bit 31: c == its old cell
+              occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokp, set31, bop3<TC & ~(TA & TB)>(mokp, clr31, occ31));
+            }
+            if (sidx + 1 < C::NAM) raw = *occ_at(cc[sidx + 1]);   // before this turn's update
+            const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
+            const uint32_t ukey = pk_min_u16(p, c) + (mul_swap(dd) << 24);   // top byte dx*dy: 1, 0xFF, 0
+            uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor is never 0
+            if constexpr (REV) {
+              const uint32_t key = (p & XY16) | ((c & XY16) << 8);
+#pragma unroll
+              for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
+            } else {
+#pragma unroll
+              for (int j = 0; j < sidx; ++j) f = min(f, xk[j] ^ ukey);
+            }
+            const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
+            const uint32_t mok = sgn(bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u));
+            atomicAnd(occ_at(p), bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
+            atomicOr(occ_at(c), bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
+            const uint32_t dxy = c ^ p;
+            if constexpr (REV) rk[sidx] = bop3<~TA | TB>(mok, (c & XY16) | ((p & XY16) << 8), 0u);
+            xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
+            const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
+            s.ag[sidx] = moved;
+            mokp = mok;
+            cp[sidx] = L.cell_row(moved);
+            if (sidx >= 1) tb[sidx - 1] = *L.row_byte(cp[sidx - 1], tid);
+            if (sidx >= 2) dst[sidx - 2] = L.dst_tb(tb[sidx - 2]);
+          }
+          // pin the hoisted block to this basic block (LLVM would sink it back to its only use)
+          if constexpr (HOIST) asm volatile("" : "+v"(rblk0.x), "+v"(rblk0.y), "+v"(rblk0.z), "+v"(rblk0.w));
+        };
+        if (!LAZY || __any(lg->cm != 0u))
+          move_loop(std::true_type{});
+        else
+          move_loop(std::false_type{});
         tb[C::NAM - 1] = *L.row_byte(cp[C::NAM - 1], tid);
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
         dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
@@ -937,7 +1000,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             ma = bop3<TA & TB>(ma, 0u - (uint32_t)valid, 0u);
             sel = select_bit64(inactive, rpos);   // positions into the inactive list, host-drawn
           } else {
-            if ((j & 1) == 0) blk = stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
+            if ((j & 1) == 0) blk = (HOIST && j == 0 && hoisted) ? rblk0 : stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
             const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
             sel = select_bit64(((uint64_t)rhi << 32) | rlo, __umulhi(w1, nin - (uint32_t)j));
             const uint32_t r2 = __umulhi(w2, (uint32_t)(C::DP - j));

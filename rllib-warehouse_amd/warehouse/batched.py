@@ -245,6 +245,18 @@ class BatchedWarehouse:
                    int(bool(autoreset)), int(self.train), self.seed, self.env_offset, self.stream)
         return obs, self.rewards, self.dones
 
+    def sampler_step(self, policy: str = "greedy", p: float = 0.0, observe: bool = True
+                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
+        """vector_step(self.policy(policy, p), autoreset=True) with the device policy fused into
+        the step launch: one 1-step wh_rollout (policy + step + auto-reset, rewards and dones into
+        the env-owned buffers) and one wh_observe -- two kernels per step instead of three, and
+        the same transitions.  Returns env-owned (obs or None, rewards [B,NA], dones [B])."""
+        self._call("wh_rollout", self.state.data_ptr(), 1, POLICIES[policy], float(p),
+                   self.rewards.data_ptr(), self.dones.data_ptr(), None,
+                   None if self.stats is None else self.stats.ref, 1, int(self.train), self.seed,
+                   self.env_offset, self.stream)
+        return (self.observe() if observe else None), self.rewards, self.dones
+
     def policy(self, kind: str = "greedy", p: float = 0.0) -> torch.Tensor:
         self._call("wh_policy", self.state.data_ptr(), POLICIES[kind], float(p), self.actions.data_ptr(),
                    self.seed, self.env_offset, self.stream)

@@ -243,6 +243,53 @@ def test_c3_full_size_shard_invariance_and_spot_check(wh):
     np.testing.assert_array_equal(full.observe().cpu().numpy()[ids], ob.observe(L, S))
 
 
+def test_c4_full_size_shard_invariance_and_spot_check(wh):
+    """Config 4 size (B=65536 Large x 16 agents, greedy, fused fast instance: the dense collision and
+    assignment path): 200 steps across an episode end; two shards of 32,768 == one batch
+    bit-exactly (rewards every step and the final state); a sampled subset of env ids equals the
+    oracle step by step; request/timer invariants hold for every env."""
+    import torch
+
+    B, seed, K = 65536, 19, 210
+    L = oc.layout_for("large")
+    full = wh.BatchedWarehouse("large", B, 16, seed=seed)
+    full.reset()
+    full.rollout(185, "greedy", 0.0)                 # untimed prefix: the window below crosses t = T
+    rew = torch.zeros((K - 185, B, 16), device=full.device)
+    dn = torch.zeros((K - 185, B), dtype=torch.uint8, device=full.device)
+    full.rollout(K - 185, "greedy", 0.0, rewards=rew, dones=dn)
+    assert int(dn.sum()) == B                         # every env ended its episode in the window
+    for h in range(2):
+        e = wh.BatchedWarehouse("large", B // 2, 16, seed=seed, env_offset=h * (B // 2))
+        e.reset()
+        e.rollout(185, "greedy", 0.0)
+        r = torch.zeros((K - 185, B // 2, 16), device=e.device)
+        d = torch.zeros((K - 185, B // 2), dtype=torch.uint8, device=e.device)
+        e.rollout(K - 185, "greedy", 0.0, rewards=r, dones=d)
+        sl = slice(h * (B // 2), (h + 1) * (B // 2))
+        torch.testing.assert_close(e.state, full.state[:, sl], rtol=0, atol=0)
+        assert torch.equal(r, rew[:, sl]) and torch.equal(d, dn[:, sl])
+        del e, r, d
+    c = canon(full)
+    active = c["pickup_target"] >= 0
+    assert (active.sum(1) == L.R).all()
+    assert ((c["pickup_timer"] >= 0) == active).all()
+    assert c["pos"].min() >= 0 and c["pos"].max() < L.D
+    ids = np.concatenate([np.random.RandomState(6).choice(B - 64, 192, replace=False), np.arange(B - 64, B)])
+    S = ob.BState.zeros(L, len(ids), 16)
+    d = ob.PhiloxDraws(seed, ids)
+    ob.reset(L, S, d)
+    rw = rew.cpu().numpy()
+    for s in range(K):
+        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, 0.0, d), d)
+        if s >= 185:
+            np.testing.assert_array_equal(rw[s - 185][ids], orew, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone)
+    assert_same({k: v[ids] for k, v in c.items()}, S, "subset")
+    np.testing.assert_array_equal(full.observe().cpu().numpy()[ids], ob.observe(L, S))
+
+
 def test_dropin_single_env_matches_reference_greedy_runs(wh):
     """Config 1 through the drop-in class on the GPU: baseline/run.py's loop, the reference solver
     (restated in oracle.core.greedy on the obs dicts), global numpy stream -> seed 0 gives 82.0."""

@@ -393,3 +393,37 @@ def test_vector_step_dict_order_masked_autoreset_vs_oracle(wh, variant, na, trai
             ob.reset(L, sub, d, mask=odone, nmax=na if train else None)
         put(S, idx, sub)
         np.testing.assert_array_equal(obs.cpu().numpy(), ob.observe(L, S), err_msg=f"obs step {s}")
+
+
+@pytest.mark.parametrize("variant,na,train,p", [("medium", 8, False, 0.0), ("medium", 9, True, 0.2), ("large", 16, False, 0.0)])
+def test_sampler_step_equals_policy_then_vector_step(wh, variant, na, train, p):
+    """BatchedWarehouse.sampler_step (the device policy fused into a 1-step wh_rollout launch, then
+    wh_observe) == wh_policy + wh_vector_step(autoreset) step by step: rewards, dones, observation
+    rows, episode metrics and the final state, over 230 steps (an episode end), and both == the
+    oracle's greedy rollout."""
+    import torch
+
+    B, seed, K = 1024, 41, 230
+    L = oc.layout_for(variant)
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    sa, sb = a.enable_episode_stats(), b.enable_episode_stats()
+    a.reset()
+    b.reset()
+    S = ob.BState.zeros(L, B, na)
+    d = ob.PhiloxDraws(seed, np.arange(B))
+    nmax = na if train else None
+    ob.reset(L, S, d, nmax=nmax)
+    for s in range(K):
+        oa, ra, da = a.sampler_step("greedy", p)
+        ob_, rb, db = b.vector_step(b.policy("greedy", p), autoreset=True)
+        assert torch.equal(ra, rb) and torch.equal(da, db) and torch.equal(oa, ob_), f"step {s}"
+        orew, odone, _, _ = ob.step(L, S, ob.greedy(L, S, p, d), d)
+        np.testing.assert_array_equal(ra.cpu().numpy(), orew, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
+        if s % 50 == 0 or s == K - 1:
+            np.testing.assert_array_equal(oa.cpu().numpy(), ob.observe(L, S), err_msg=f"obs step {s}")
+    assert torch.equal(a.state, b.state)
+    for k in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
+        assert torch.equal(getattr(sa, k), getattr(sb, k)), k
