@@ -181,6 +181,15 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream);
 
+/* One step of the sampler route with the device policy (the greedy solver of baseline/solvers.py:27-58
+ * standing in for the learner's policy, or uniform random actions): policy + step + auto-reset
+ * (Train variants redraw n) in one step launch, then the observation rows (wh_observe); the same
+ * philox draws and results as wh_policy followed by wh_vector_step(autoreset = 1), one launch
+ * fewer.  rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats may be NULL. */
+int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t policy, float p,
+                    float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats,
+                    int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
+
 /* A prepared wh_rollout: the same arguments resolved once (config validated, kernel and tables
  * chosen) into an opaque handle, so a loop that launches the same rollout repeatedly pays one
  * cheap call per launch (wh_launch_run enqueues exactly what wh_rollout would).  The buffers must

@@ -54,6 +54,13 @@ constexpr bool kBiasAddr = true;
 #else
 constexpr bool kBiasAddr = false;
 #endif
+// -DWH_OBS_NT: observation rows stored nontemporal (A/B: 5 % slower at Medium-8 and Large-16, 5 %
+// faster at Small-4, same box; tools/obs_bench.py)
+#ifdef WH_OBS_NT
+constexpr bool kObsNT = true;
+#else
+constexpr bool kObsNT = false;
+#endif
 #ifndef WH_NO_REGEN_HOIST
 constexpr bool kRegenHoist = true;
 #else
@@ -89,6 +96,7 @@ struct Cfg {
 };
 
 typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 __device__ __forceinline__ uint32_t as_u(short2v v) { return __builtin_bit_cast(uint32_t, v); }
 
@@ -341,26 +349,42 @@ __device__ __forceinline__ void load_env_issue(RawEnv<C>& r, const uint32_t* __r
   for (int w = 0; w < C::PW; ++w) r.pm[w] = st[(wpt + C::PW + w) * B + e];
 }
 
+// SWAR byte ops on 4 packed unsigned bytes (H = the bytes' high bits)
+constexpr uint32_t SWAR_H = 0x80808080u;
+__device__ __forceinline__ uint32_t swar_sub(uint32_t x, uint32_t y) {   // (x_b - y_b) mod 256 per byte
+  return ((x | SWAR_H) - (y & ~SWAR_H)) ^ ((x ^ ~y) & SWAR_H);
+}
+__device__ __forceinline__ uint32_t swar_lt(uint32_t x, uint32_t y) {    // bit 7 of byte b: x_b < y_b
+  return (((~x & y) | (~(x ^ y) & swar_sub(x, y))) & SWAR_H);
+}
+
 template <class C>
 __device__ __forceinline__ void load_env_finish(Regs<C>& s, Lds<C>& L, const RawEnv<C>& r, uint32_t W, int tid) {
   s.hdr = r.hdr;
   s.epi = r.epi;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) s.ag[i] = r.ag[i];
+  // pickup cell j = target byte | expiry byte << 8: two cells per v_perm, stored as 16-bit halves
 #pragma unroll
-  for (int j = 0; j < C::P; ++j)
-    L.pkp[j][tid] = (uint16_t)(((r.pt[j >> 2] >> (8 * (j & 3))) & 0xFFu) | (((r.pm[j >> 2] >> (8 * (j & 3))) & 0xFFu) << 8));
-  s.am = active_mask<C>(r.pt);
-  // expiry step of each open request: t + (expiry byte - t) mod 256, as the expiry phase counts
-  const uint32_t t0 = s.hdr & 0xFFFFu;
-  bool early = false;
-#pragma unroll
-  for (int j = 0; j < C::P; ++j) {
-    const uint32_t sh = 8 * (j & 3);
-    const uint32_t rem = (((r.pm[j >> 2] >> sh) & 0xFFu) - t0) & 0xFFu;
-    early |= ((r.pt[j >> 2] >> sh) & 0xFFu) != 0u && t0 + rem < W;
+  for (int w = 0; w < C::PW; ++w) {
+    const uint32_t lo = __builtin_amdgcn_perm(r.pm[w], r.pt[w], 0x05010400u);   // cells 4w, 4w+1
+    const uint32_t hi = __builtin_amdgcn_perm(r.pm[w], r.pt[w], 0x07030602u);   // cells 4w+2, 4w+3
+    L.pkp[4 * w][tid] = (uint16_t)lo;
+    L.pkp[4 * w + 1][tid] = (uint16_t)(lo >> 16);
+    L.pkp[4 * w + 2][tid] = (uint16_t)hi;
+    L.pkp[4 * w + 3][tid] = (uint16_t)(hi >> 16);
   }
-  s.wskip = __any(early) ? 0u : W;
+  s.am = active_mask<C>(r.pt);
+  // An open request expires at step t0 + ((expiry byte - t0) mod 256), as the expiry phase counts;
+  // it is "early" if that is before W, i.e. its steps left < W - t0 (never when t0 >= W).  Four
+  // points per SWAR test.
+  const uint32_t t0 = s.hdr & 0xFFFFu;
+  const uint32_t thr = t0 < W ? W - t0 : 0u;          // <= 255
+  uint32_t early = 0;
+#pragma unroll
+  for (int w = 0; w < C::PW; ++w)
+    early |= nz_hi(r.pt[w]) & swar_lt(swar_sub(r.pm[w], (t0 & 0xFFu) * 0x01010101u), thr * 0x01010101u);
+  s.wskip = __any(early != 0u) ? 0u : W;
 }
 
 template <class C>
@@ -374,15 +398,11 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
   const int wpt = 2 + na;
 #pragma unroll
   for (int w = 0; w < C::PW; ++w) {
-    uint32_t pt = 0, pm = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t v = L.pkp[4 * w + b][tid];
-      pt |= (v & 0xFFu) << (8 * b);
-      pm |= (v >> 8) << (8 * b);
-    }
-    st[(wpt + w) * B + e] = pt;
-    st[(wpt + C::PW + w) * B + e] = pm;
+    // four 16-bit cells -> target bytes and expiry bytes: two shift-ors and two v_perm
+    const uint32_t lo = (uint32_t)L.pkp[4 * w][tid] | ((uint32_t)L.pkp[4 * w + 1][tid] << 16);
+    const uint32_t hi = (uint32_t)L.pkp[4 * w + 2][tid] | ((uint32_t)L.pkp[4 * w + 3][tid] << 16);
+    st[(wpt + w) * B + e] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+    st[(wpt + C::PW + w) * B + e] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
   }
 }
 
@@ -1048,6 +1068,31 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   return done;
 }
 
+// Image offset of output value f of agent row i (sorted-key order, see wh_observe).
+// Image layout: [0] n, [A0 + r] availability of agent r, [G0 + 2r] its delivery target (x, y),
+// [P0 + 2r] its position (x, y), [Q0 + 4q] request q (pickup x, y, delivery x, y); k_observe's
+// byte image packs the sections back to back (the defaults).
+template <int R, int A0 = 1, int G0 = 1 + R, int P0 = 1 + 3 * R, int Q0 = 1 + 5 * R>
+__host__ __device__ constexpr uint32_t obs_src(int i, int f, bool fresh) {
+  if (f == 0) return 0;                                                    // num_agents
+  if (f < R) {                                                             // other_availabilities
+    const int j = f - 1;
+    return A0 + (j < i ? j : j + 1);
+  }
+  if (f < 3 * R - 2) {                                                     // other_delivery_targets
+    const int k = f - R, j = k >> 1, drop = fresh ? i : 1;
+    return G0 + 2 * (j < drop ? j : j + 1) + (k & 1);
+  }
+  if (f < 5 * R - 4) {                                                     // other_positions
+    const int k = f - (3 * R - 2), j = k >> 1;
+    return P0 + 2 * (j < i ? j : j + 1) + (k & 1);
+  }
+  if (f < 9 * R - 4) return Q0 + (f - (5 * R - 4));                        // requests
+  if (f == 9 * R - 4) return A0 + i;                                       // self_availability
+  if (f < 9 * R - 1) return G0 + 2 * i + (f - (9 * R - 3));                // self_delivery_target
+  return P0 + 2 * i + (f - (9 * R - 1));                                   // self_position
+}
+
 // ----------------------------------------------------------------------------- kernels
 // rewards[B, na]: a wave's 64 envs own one contiguous block of 64*na floats.  Even agent counts
 // store each lane's row with 16/8-byte stores; otherwise lanes write their rows into LDS (the agl
@@ -1435,30 +1480,6 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
 // 16 lanes per env, then writes the group's contiguous [16 env x na x L] float region as float4s.
 // Small workgroups keep many groups in flight per CU, so one group's image build overlaps the
 // others' streaming stores.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Image offset of output value f of agent row i (sorted-key order, see wh_observe).
-template <int R>
-__host__ __device__ constexpr uint32_t obs_src(int i, int f, bool fresh) {
-  constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
-  if (f == 0) return 0;                                                    // num_agents
-  if (f < R) {                                                             // other_availabilities
-    const int j = f - 1;
-    return A0 + (j < i ? j : j + 1);
-  }
-  if (f < 3 * R - 2) {                                                     // other_delivery_targets
-    const int k = f - R, j = k >> 1, drop = fresh ? i : 1;
-    return G0 + 2 * (j < drop ? j : j + 1) + (k & 1);
-  }
-  if (f < 5 * R - 4) {                                                     // other_positions
-    const int k = f - (3 * R - 2), j = k >> 1;
-    return P0 + 2 * (j < i ? j : j + 1) + (k & 1);
-  }
-  if (f < 9 * R - 4) return Q0 + (f - (5 * R - 4));                        // requests
-  if (f == 9 * R - 4) return A0 + i;                                       // self_availability
-  if (f < 9 * R - 1) return G0 + 2 * i + (f - (9 * R - 3));                // self_delivery_target
-  return P0 + 2 * i + (f - (9 * R - 1));                                   // self_position
-}
 
 template <int R, int NAM>
 struct ObsSrc {
@@ -1594,7 +1615,10 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
         }
         w[jj] = hv[0] | (hv[1] << 16);
       }
-      out[c] = make_uint4(w[0], w[1], w[2], w[3]);
+      typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+      const u32x4v v = {w[0], w[1], w[2], w[3]};
+      if constexpr (kObsNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(&out[c]));
+      else *reinterpret_cast<u32x4v*>(&out[c]) = v;
     }
   }
   if (!obs) return;
@@ -1604,6 +1628,8 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
     const uint32_t qe = per_env >> 2, total = nenv * qe;
     const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
     f32x4* out4 = reinterpret_cast<f32x4*>(out);
+    // (unrolling this loop 2x or 4x, reads of a pass issued together, measured no faster: it is
+    // write-bound, tools/obs_bench.py)
     for (uint32_t q = tid; q < total; q += BT) {
       const uint32_t el4 = __umulhi(q, magic);
       const uint32_t k4 = q - el4 * qe;
@@ -1616,7 +1642,8 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
       v.y = live > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
       v.z = live > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
       v.w = live > 3 ? (float)im[sw >> 24] : 0.0f;
-      out4[q] = v;
+      if constexpr (kObsNT) __builtin_nontemporal_store(v, &out4[q]);
+      else out4[q] = v;
     }
   } else {
     const uint32_t total = nenv * per_env;
@@ -1885,6 +1912,8 @@ Kernels make_kernels() {
 const std::vector<Kernels>& registry() {
 #ifdef WH_ONLY_MEDIUM8   // analysis builds (tools/lds_stalls.py): one instance, fast to compile
   static const std::vector<Kernels> r = {make_kernels<16, 9, 3, 8>()};
+#elif defined(WH_ONLY_LARGE16)
+  static const std::vector<Kernels> r = {make_kernels<20, 16, 4, 16>()};
 #else
   static const std::vector<Kernels> r = {
       // WarehouseSmall  (variants.py:19-32): D=12, R=4, racks [4, 8]
@@ -2238,6 +2267,32 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
   a.variable_n = variable_n ? 1 : 0;
   if (stats) a.stats = *stats;
   int rc = launch_step(cfg, B, state, POL_EXTERNAL, a, stream);
+  if (rc || !obs) return rc;
+  return wh_observe(cfg, B, state, obs, stream);
+}
+
+int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t policy, float p,
+                    float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats,
+                    int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream) {
+  if (policy != WH_POLICY_GREEDY && policy != WH_POLICY_RANDOM) return WH_EINVAL;
+  if (!(p >= 0.0f && p <= 1.0f) || !stats_ok(stats)) return WH_EINVAL;
+  StepParams a{};
+  if (stats) a.stats = *stats;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.p = p;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = 1;
+  a.phase = PH_ALL;
+  a.autoreset = 1;
+  a.variable_n = variable_n ? 1 : 0;
+  // the step launch (the fused rollout instance when its outputs allow) and the observation
+  // kernel: a step launch holds one workgroup per CU, too few waves to stream 2.6 KB of rows per
+  // env near the write ceiling (measured: 2.7 TB/s as an epilogue of the step launch against
+  // k_observe's 5.7 TB/s), so the rows stay with k_observe's small workgroups
+  int rc = launch_step(cfg, B, state, policy, a, stream);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
 }

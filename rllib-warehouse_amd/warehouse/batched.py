@@ -248,14 +248,18 @@ class BatchedWarehouse:
     def sampler_step(self, policy: str = "greedy", p: float = 0.0, observe: bool = True
                      ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
         """vector_step(self.policy(policy, p), autoreset=True) with the device policy fused into
-        the step launch: one 1-step wh_rollout (policy + step + auto-reset, rewards and dones into
-        the env-owned buffers) and one wh_observe -- two kernels per step instead of three, and
-        the same transitions.  Returns env-owned (obs or None, rewards [B,NA], dones [B])."""
-        self._call("wh_rollout", self.state.data_ptr(), 1, POLICIES[policy], float(p),
-                   self.rewards.data_ptr(), self.dones.data_ptr(), None,
-                   None if self.stats is None else self.stats.ref, 1, int(self.train), self.seed,
+        the step launch (wh_sampler_step: policy + step + auto-reset, then the observation rows),
+        with the same transitions and rows and one launch fewer.
+        Returns env-owned (obs [B,NA,9R+1] or None, rewards [B,NA], dones [B])."""
+        if observe and self._obs is None:
+            self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
+                                    device=self.device)
+        obs = self._obs if observe else None
+        self._call("wh_sampler_step", self.state.data_ptr(), POLICIES[policy], float(p),
+                   self.rewards.data_ptr(), self.dones.data_ptr(), nat.ptr(obs),
+                   None if self.stats is None else self.stats.ref, int(self.train), self.seed,
                    self.env_offset, self.stream)
-        return (self.observe() if observe else None), self.rewards, self.dones
+        return obs, self.rewards, self.dones
 
     def policy(self, kind: str = "greedy", p: float = 0.0) -> torch.Tensor:
         self._call("wh_policy", self.state.data_ptr(), POLICIES[kind], float(p), self.actions.data_ptr(),

@@ -427,3 +427,28 @@ def test_sampler_step_equals_policy_then_vector_step(wh, variant, na, train, p):
     assert torch.equal(a.state, b.state)
     for k in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
         assert torch.equal(getattr(sa, k), getattr(sb, k)), k
+
+
+@pytest.mark.parametrize("variant,na,train,B", [("medium", 8, False, 4096), ("medium", 9, True, 1000),
+                                                ("large", 16, False, 777), ("large", 5, False, 300),
+                                                ("small", 4, True, 2049), ("small", 3, False, 129)])
+def test_sampler_observation_rows_equal_wh_observe(wh, variant, na, train, B):
+    """The observation rows wh_vector_step and wh_sampler_step return are wh_observe's on the
+    state they leave: masked steps, ragged batches (a partial last workgroup), odd agent counts
+    (rows not a multiple of 4 floats), Train variants, fresh resets."""
+    import torch
+
+    env = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=3)
+    env.reset()
+    g = torch.Generator(device=env.device).manual_seed(1)
+    NA = env.agent_slots
+    for s in range(260):
+        if s % 3 == 0:
+            acts = torch.randint(0, 9, (B, NA), device=env.device, dtype=torch.int32, generator=g)
+            mask = (torch.rand(B, device=env.device, generator=g) < 0.5) if s % 2 else None
+            obs, _, _ = env.vector_step(acts, autoreset=True, mask=mask)
+        else:
+            obs, _, _ = env.sampler_step("greedy", 0.1 if s % 2 else 0.0)
+        fused = obs.clone()
+        ref = env.observe()
+        assert torch.equal(fused, ref), f"step {s}"
