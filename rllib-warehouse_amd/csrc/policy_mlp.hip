@@ -379,6 +379,8 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
         stream_ops<N::L1OPS, 4, N::XPF ? 1 : 2>(stage_of(g), lane, [&](int i, bf16x8 af) {
           const int nn = i / N::U1, k = i % N::U1;
           if (k < 2 * N::T0) {
+            // (one chain per tile: splitting it into two accumulators, even / odd k-steps, measured
+            // 2-6 % slower -- the dependent MFMAs are not what binds)
             acc = mfma(af, hb[k >> 1][k & 1], k == 0 ? f32x16{} : acc);
             if (k == 2 * N::T0 - 1) {
               if (MLP_ABL(a, 2)) raw_frags(acc, f0, f1);

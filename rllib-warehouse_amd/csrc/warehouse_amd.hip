@@ -61,6 +61,13 @@ constexpr bool kObsNT = true;
 #else
 constexpr bool kObsNT = false;
 #endif
+#ifndef WH_REV_SPLIT_MAX_NAM   // agent counts up to which the move loop has the no-reverse-key variant
+#define WH_REV_SPLIT_MAX_NAM 9     // (Large-16, whose step loop spills, measured 1 % slower with it)
+#endif
+#ifndef WH_BIAS_MAX_NAM
+#define WH_BIAS_MAX_NAM 64
+#endif
+constexpr int kRevSplitMaxNam = WH_REV_SPLIT_MAX_NAM, kBiasMaxNam = WH_BIAS_MAX_NAM;
 #ifndef WH_NO_REGEN_HOIST
 constexpr bool kRegenHoist = true;
 #else
@@ -758,6 +765,29 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     uint32_t cp[C::NAM], tb[C::NAM], dst[C::NAM];   // pickup lookups (core.py:309-329): cell_row,
                                                     // target byte, delivery cell
     bool looked = false;
+    // pickups (core.py:309-335): agent i takes iff it stands on a pickup point (cp != 0) with an
+    // open request (tb != 0) and is idle -- slots >= n sit idle on the corner cell (0, 0), which is
+    // no pickup point; min3 of the three 0/1-ish terms is 1 exactly when all hold.  Every agent
+    // decides against the pre-pickup table (two agents on one point both take it), so the
+    // points are cleared only after every agent's target byte has been read (clr[i]: the byte to
+    // zero, row P = scratch).  The ascending move loop decides each agent three turns after its
+    // move, when its lookups have landed, so only a few agents' lookups are live at a time.
+    uint64_t picked = 0;
+    uint32_t clr[C::NAM];
+    auto pick = [&](int i, uint32_t cpv, uint32_t tbv, uint32_t dstv) {
+      const uint32_t a = s.ag[i];
+      const uint32_t idle01 = (a >> 15) & 1u;   // delivery-target byte 0xFF
+      const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cpv, tbv), idle01);
+      s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dstv << 8, IDLE);   // idle target bytes are 0xFF
+      picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cpv / ROWB - 1u) & 63u);
+      clr[i] = msel(m, cpv, (uint32_t)(C::P + 1) * ROWB);
+      rewm[i] = m;
+    };
+#ifndef WH_NO_PICK_IN_LOOP   // (A/B builds: -DWH_NO_PICK_IN_LOOP decides after the move loop)
+    constexpr bool PICK_IN_LOOP = true;
+#else
+    constexpr bool PICK_IN_LOOP = false;
+#endif
     if (!(ablate & 2)) {
       // The grid is rebuilt as {live agents' cells} (core.py:275-276) by OR-ing the cells into
       // what the previous step left, which is always a subset of them (a set bit is an arrival
@@ -856,7 +886,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         // occ[y][lane] (y * 1024 + lane * 4; x < 32) -- one shift per LDS address instead of a
         // field extract and a shift-or.  Equality tests, x-bit selects and the square key's
         // packed minimum are unaffected (every position of a lane carries the same lane bits).
-        constexpr bool BIAS = !CLAMP && kBiasAddr;
+        constexpr bool BIAS = !CLAMP && kBiasAddr && C::NAM <= kBiasMaxNam;
         static_assert(BT * 4 == 1024 && C::D <= 32, "occ[y][lane] = byte y << 10 | lane << 2");
         const uint32_t lbias = BIAS ? ((uint32_t)tid & 255u) << 8 : 0u;
         auto occ_at = [&](uint32_t q) -> uint32_t* {
@@ -932,17 +962,22 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             cp[sidx] = L.cell_row(moved);
             if (sidx >= 1) tb[sidx - 1] = *L.row_byte(cp[sidx - 1], tid);
             if (sidx >= 2) dst[sidx - 2] = L.dst_tb(tb[sidx - 2]);
+            if (PICK_IN_LOOP && !(ablate & 8) && sidx >= 3) pick(sidx - 3, cp[sidx - 3], tb[sidx - 3], dst[sidx - 3]);
           }
           // pin the hoisted block to this basic block (LLVM would sink it back to its only use)
           if constexpr (HOIST) asm volatile("" : "+v"(rblk0.x), "+v"(rblk0.y), "+v"(rblk0.z), "+v"(rblk0.w));
         };
-        if (!LAZY || __any(lg->cm != 0u))
+        if (!LAZY || C::NAM > kRevSplitMaxNam || __any(lg->cm != 0u))
           move_loop(std::true_type{});
         else
           move_loop(std::false_type{});
         tb[C::NAM - 1] = *L.row_byte(cp[C::NAM - 1], tid);
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
         dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
+        if (PICK_IN_LOOP && !(ablate & 8)) {
+#pragma unroll
+          for (int i = (C::NAM > 3 ? C::NAM - 3 : 0); i < C::NAM; ++i) pick(i, cp[i], tb[i], dst[i]);
+        }
         looked = true;
         if (LAZY && __any(lg->cm != 0u)) {   // did an agent that shares a cell move?
           uint32_t acc = 0;
@@ -966,21 +1001,12 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) dst[i] = L.dst_tb(tb[i]);
       }
-      uint64_t picked = 0;
+      if (!looked || !PICK_IN_LOOP) {
 #pragma unroll
-      for (int i = 0; i < C::NAM; ++i) {
-        // take iff on a pickup point (cp != 0) with an open request (tb != 0) and idle: slots >= n
-        // sit idle on the corner cell (0, 0), which is no pickup point.  min3 of the three 0/1-ish
-        // terms is 1 exactly when all hold.
-        // The point is cleared right away: every agent's target byte was read before this loop.
-        const uint32_t a = s.ag[i];
-        const uint32_t idle01 = (a >> 15) & 1u;   // delivery-target byte 0xFF
-        const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cp[i], tb[i]), idle01);
-        s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dst[i] << 8, IDLE);   // idle target bytes are 0xFF
-        picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cp[i] / ROWB - 1u) & 63u);
-        *L.row_byte(msel(m, cp[i], (uint32_t)(C::P + 1) * ROWB), tid) = 0;   // row P: scratch
-        rewm[i] = m;
+        for (int i = 0; i < C::NAM; ++i) pick(i, cp[i], tb[i], dst[i]);
       }
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) *L.row_byte(clr[i], tid) = 0;
       s.am &= ~picked;
     }
   }

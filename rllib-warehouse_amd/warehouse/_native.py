@@ -108,34 +108,46 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C rllib-warehouse_amd/csrc` (there is no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
-    L.wh_version.restype = ctypes.c_char_p
-    L.wh_version.argtypes = []
-    L.wh_query.argtypes = [_CFG, ctypes.POINTER(WhLayout)]
-    L.wh_pack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
-    L.wh_unpack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
-    L.wh_reset.argtypes = [_CFG, _I64, _P, _P, ctypes.POINTER(WhResetDraws), _I32, _U64, _I64, _P]
-    L.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P]
-    L.wh_observe.argtypes = [_CFG, _I64, _P, _P, _P]
-    L.wh_observe_x.argtypes = [_CFG, _I64, _P, _P, _P, _P]
-    L.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
+
+    class _Sigs:   # argtypes for the exported symbols (an A/B build of another version may lack some)
+        def __setattr__(self, name, val):
+            pass
+
+    class _Lib:
+        def __getattr__(self, name):
+            try:
+                return getattr(L, name)
+            except AttributeError:
+                return _Sigs()
+    S = _Lib()
+    S.wh_version.restype = ctypes.c_char_p
+    S.wh_version.argtypes = []
+    S.wh_query.argtypes = [_CFG, ctypes.POINTER(WhLayout)]
+    S.wh_pack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
+    S.wh_unpack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
+    S.wh_reset.argtypes = [_CFG, _I64, _P, _P, ctypes.POINTER(WhResetDraws), _I32, _U64, _I64, _P]
+    S.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P]
+    S.wh_observe.argtypes = [_CFG, _I64, _P, _P, _P]
+    S.wh_observe_x.argtypes = [_CFG, _I64, _P, _P, _P, _P]
+    S.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
     _ST = ctypes.POINTER(WhEpisodeStats)
-    L.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
-    L.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
-    L.wh_sampler_step.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]
+    S.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    S.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    S.wh_sampler_step.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]
     _MD = ctypes.POINTER(WhMlpDesc)
-    L.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
-    L.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
-    L.wh_mlp_forward.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
-    L.wh_mlp_forward_x.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
-    L.wh_check_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), _I32]
-    L.wh_rollout_prepare.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P,
+    S.wh_mlp_query.argtypes = [_MD, ctypes.POINTER(ctypes.c_int64)]
+    S.wh_mlp_pack.argtypes = [_MD] + [_P] * 7
+    S.wh_mlp_forward.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
+    S.wh_mlp_forward_x.argtypes = [_MD, _P, _I64, _P, _P, _P, _I32, _U64, ctypes.c_uint32, _P]
+    S.wh_check_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), _I32]
+    S.wh_rollout_prepare.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P,
                                      ctypes.POINTER(ctypes.c_void_p)]
-    L.wh_launch_run.argtypes = [_P]
-    L.wh_launch_run_timed.argtypes = [_P, _P, _P]
-    L.wh_launch_free.argtypes = [_P]
-    L.wh_launch_free.restype = None
+    S.wh_launch_run.argtypes = [_P]
+    S.wh_launch_run_timed.argtypes = [_P, _P, _P]
+    S.wh_launch_free.argtypes = [_P]
+    S.wh_launch_free.restype = None
     for name in SYMBOLS:
-        if name != "wh_version":
+        if name not in ("wh_version", "wh_launch_free") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -17,14 +17,22 @@ for abl, variant, na in [(a, v, n) for a in os.environ.get("MLP_ABLATE", "0").sp
     rows = B * na
     x = torch.randn((rows, net.in_dim), device="cuda") * 4
     acts = torch.empty(rows, dtype=torch.int32, device="cuda")
+    if os.environ.get("MLP_X") == "1":
+        # the fragment-order operand (wh_observe_x's layout): random bf16 of magnitude [0.5, 1)
+        kq = (net.in_dim + 2 + 15) // 16
+        bits = torch.randint(0, 1 << 15, ((rows + 31) // 32, kq, 64, 8), device="cuda", dtype=torch.int32)
+        xf = ((bits & 0x807F) | 0x3F00).to(torch.int16).view(torch.uint8).contiguous()
+        fwd = lambda: net.forward_x(xf, rows, actions=acts, step=0)   # noqa: E731
+    else:
+        fwd = lambda: net(x, actions=acts, step=0)   # noqa: E731
     for _ in range(3):
-        net(x, actions=acts, step=0)
+        fwd()
     torch.cuda.synchronize()
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 10
     t0.record()
     for _ in range(reps):
-        net(x, actions=acts, step=0)
+        fwd()
     t1.record()
     torch.cuda.synchronize()
     us = t0.elapsed_time(t1) / reps * 1e3
