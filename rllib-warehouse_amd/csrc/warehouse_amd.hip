@@ -62,8 +62,12 @@ constexpr bool kObsNT = true;
 constexpr bool kObsNT = false;
 #endif
 #ifndef WH_REV_SPLIT_MAX_NAM   // agent counts up to which the move loop has the no-reverse-key variant
-#define WH_REV_SPLIT_MAX_NAM 9     // (Large-16, whose step loop spills, measured 1 % slower with it)
+#define WH_REV_SPLIT_MAX_NAM 9
 #endif
+#ifndef WH_UKEY_MIN_NAM        // agent counts from which the ascending move loop uses one key per move
+#define WH_UKEY_MIN_NAM 0      // (A/B builds: 99 = the two-key form with its reverse-key split)
+#endif
+constexpr int kUKeyMinNam = WH_UKEY_MIN_NAM;
 #ifndef WH_BIAS_MAX_NAM
 #define WH_BIAS_MAX_NAM 64
 #endif
@@ -678,6 +682,10 @@ struct LazyGrid {
   uint32_t cm;    // slots sharing a cell (found by the last rebuild or reset): rebuild once one moves
 };
 
+#ifdef WH_COUNT_REV
+__device__ unsigned long long g_wh_revcount[2];   // [0] reverse-key loops, [1] crossing-only loops
+#endif
+
 template <class C, bool ORDERED, bool INJ = true, bool CLAMP = true, bool LAZY = false>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
                                          const int32_t* __restrict__ order,
@@ -917,6 +925,23 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         // lanes with shared cells (lg->cm, from the last rebuild; new sharing needs an existing
         // one), so a wave with none of them tests the crossing keys only -- one xor per earlier
         // agent, reduced three at a time, instead of two xors and a min3.
+        //
+        // UKEY: one key per move and ONE test per earlier agent, exact in every lane, so there is a
+        // single loop variant.  A unit move p -> c is keyed by its undirected edge or
+        // square, u = p + c per coordinate (x and y sums; a stay has both even, an axis move one odd,
+        // a diagonal both odd -- and both diagonals of a square share it), and by its direction
+        // (dx, dy) bytes: K = dx | dy << 8 | xsum << 16 | ysum << 24.  The moves an accepted move
+        // forbids (core.py:293-297) are exactly those with its u and another direction -- its
+        // reverse, and for a diagonal the two directions of the other diagonal -- so agent i is
+        // blocked iff some stored key S_j has 1 <= (K_i ^ S_j) <= 0xFFFF: one v_xad ((K ^ S) - 1)
+        // and half a v_min3 per pair against a cap of 0xFFFF.  An accepted stay adds its own key
+        // (p, p) to the reference's set (it can be accepted where a co-located agent left the cell):
+        // its stored key has the low bit flipped, so a later stay on that cell lands on 1.  A
+        // rejected move stores ~0 (its high bytes never match: sums <= 62).  Same-box A/B against
+        // the two-key form below (reverse-key split): 200-step launches Large-16 -10 %, Medium-8
+        // -5 % (at Large the split variant made the step loop spill in its common path).
+        constexpr bool UKEY = C::NAM >= kUKeyMinNam;
+        uint32_t sk[C::NAM];
         auto move_loop = [&](auto rev_tag) {
           constexpr bool REV = decltype(rev_tag)::value;
           if constexpr (HOIST) {   // (an opaque zero keeps LLVM from hoisting it above the branch)
@@ -939,23 +964,38 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             }
             if (sidx + 1 < C::NAM) raw = *occ_at(cc[sidx + 1]);   // before this turn's update
             const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
-            const uint32_t ukey = pk_min_u16(p, c) + (mul_swap(dd) << 24);   // top byte dx*dy: 1, 0xFF, 0
+            uint32_t ukey, kpr = 0;
             uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor is never 0
-            if constexpr (REV) {
-              const uint32_t key = (p & XY16) | ((c & XY16) << 8);
+            if constexpr (UKEY) {
+              kpr = __builtin_amdgcn_perm(as_u(as_s2(p) + as_s2(c)), dd, 0x06040200u);
+              f = 0xFFFFu;
 #pragma unroll
-              for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
+              for (int j = 0; j < sidx; ++j) f = min(f, (kpr ^ sk[j]) - 1u);
+              f -= 0xFFFEu;   // bit 31 of f - 1 below: blocked (f was < 0xFFFF)
             } else {
+              ukey = pk_min_u16(p, c) + (mul_swap(dd) << 24);   // top byte dx*dy: 1, 0xFF, 0
+              if constexpr (REV) {
+                const uint32_t key = (p & XY16) | ((c & XY16) << 8);
 #pragma unroll
-              for (int j = 0; j < sidx; ++j) f = min(f, xk[j] ^ ukey);
+                for (int j = 0; j < sidx; ++j) f = min(f, min(rk[j] ^ key, xk[j] ^ ukey));
+              } else {
+#pragma unroll
+                for (int j = 0; j < sidx; ++j) f = min(f, xk[j] ^ ukey);
+              }
             }
             const uint32_t live31 = (uint32_t)sidx - n;                 // bit 31: sidx < n
             const uint32_t mok = sgn(bop3<TA & ~TB & ~TC>(live31, occ31, f - 1u));
             atomicAnd(occ_at(p), bop3<~(TA & TB)>(mok, 1u << (p & 31u), 0u));
             atomicOr(occ_at(c), bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
             const uint32_t dxy = c ^ p;
-            if constexpr (REV) rk[sidx] = bop3<~TA | TB>(mok, (c & XY16) | ((p & XY16) << 8), 0u);
-            xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
+            if constexpr (UKEY) {
+              uint32_t z;   // 1 for a stay: v_ffbl of 0 is ~0
+              asm("v_ffbl_b32 %0, %1" : "=v"(z) : "v"(dd));
+              sk[sidx] = bop3<~TA | (TB ^ TC)>(mok, kpr, z >> 31);
+            } else {
+              if constexpr (REV) rk[sidx] = bop3<~TA | TB>(mok, (c & XY16) | ((p & XY16) << 8), 0u);
+              xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
+            }
             const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
             s.ag[sidx] = moved;
             mokp = mok;
@@ -967,10 +1007,22 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           // pin the hoisted block to this basic block (LLVM would sink it back to its only use)
           if constexpr (HOIST) asm volatile("" : "+v"(rblk0.x), "+v"(rblk0.y), "+v"(rblk0.z), "+v"(rblk0.w));
         };
-        if (!LAZY || C::NAM > kRevSplitMaxNam || __any(lg->cm != 0u))
+#ifdef WH_FORCE_NOREV   // timing-only A/B builds: never the reverse-key loop (wrong with co-located agents)
+        if (!LAZY && !UKEY)
+#else
+        if (!UKEY && (!LAZY || C::NAM > kRevSplitMaxNam || __any(lg->cm != 0u)))
+#endif
+        {
+#ifdef WH_COUNT_REV   // A/B builds: count the wave-steps that take the reverse-key loop (wh_check_read)
+          if (LAZY && __lane_id() == 0) atomicAdd(&g_wh_revcount[0], 1ull);
+#endif
           move_loop(std::true_type{});
-        else
+        } else {
+#ifdef WH_COUNT_REV
+          if (__lane_id() == 0) atomicAdd(&g_wh_revcount[1], 1ull);
+#endif
           move_loop(std::false_type{});
+        }
         tb[C::NAM - 1] = *L.row_byte(cp[C::NAM - 1], tid);
         if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
         dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
@@ -1991,6 +2043,21 @@ int wh_check_read(uint64_t* out, int32_t clear) {
   if (clear) {
     const unsigned long long z[4] = {0, 0, 0, 0};
     he = hipMemcpyToSymbol(HIP_SYMBOL(g_wh_check), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    if (he != hipSuccess) return hip_err(he);
+  }
+  return WH_OK;
+#elif defined(WH_COUNT_REV)
+  if (!out) return WH_EINVAL;
+  unsigned long long v[2];
+  hipError_t he = hipDeviceSynchronize();
+  if (he == hipSuccess) he = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_wh_revcount), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (he != hipSuccess) return hip_err(he);
+  out[0] = v[0];
+  out[1] = v[1];
+  out[2] = out[3] = 0;
+  if (clear) {
+    const unsigned long long z[2] = {0, 0};
+    he = hipMemcpyToSymbol(HIP_SYMBOL(g_wh_revcount), z, sizeof(z), 0, hipMemcpyHostToDevice);
     if (he != hipSuccess) return hip_err(he);
   }
   return WH_OK;
