@@ -85,9 +85,9 @@ constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 struct TableLayout {
   int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
-      : cell(0), rp(512 * D), tag(512 * D + 4), dst(512 * D + 8 * (P + 1)),   // rp/tag interleaved
-        mv(512 * D + 8 * (P + 1) + 4 * DP), valid(512 * D + 8 * (P + 1) + 4 * DP + 48),
-        bytes(512 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
+      : cell(0), rp(256 * D), tag(256 * D + 4), dst(256 * D + 8 * (P + 1)),   // rp/tag interleaved
+        mv(256 * D + 8 * (P + 1) + 4 * DP), valid(256 * D + 8 * (P + 1) + 4 * DP + 48),
+        bytes(256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
 
 template <int D_, int R_, int NR_, int NAM_>
@@ -274,18 +274,16 @@ struct Lds {
   // Agent words when processing in action-dict order; afterwards the reward-row staging area.
   // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
   alignas(16) uint32_t agl[C::NAM][BT];
-  // Cell (x | y << 16) -> (pickup index + 1) * ROWB, 0 for other cells: the byte offset of the
-  // point's row in pkp, counted from the row before it, so a lookup is one v_perm + one ds_read
-  // and the dependent target read one add.
+  // Cell (x | y << 16) -> pickup index + 1, 0 for other cells: one v_perm (the byte index
+  // x | y << 8) + one ds_read_u8; the point's row in pkp is then one v_lshl_add away (row_byte).
   __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
-    return reinterpret_cast<const uint16_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
+    return reinterpret_cast<const uint8_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
   }
 
   // (pickup cell, greedy tag) of point j: one 8-byte LDS read
   __device__ __forceinline__ uint2 rtag(uint32_t j) const {
     return reinterpret_cast<const uint2*>(&tbl[C::T.rp / 4])[j];
   }
-  __device__ __forceinline__ uint32_t dst(uint32_t d) const { return tbl[C::T.dst / 4 + d]; }
   __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
   __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
   __device__ __forceinline__ uint32_t target_byte(uint32_t j, int tid) const {
@@ -294,17 +292,20 @@ struct Lds {
   __device__ __forceinline__ void clear_target(uint32_t j, int tid) {
     *reinterpret_cast<uint8_t*>(&pkp[j][tid]) = 0;
   }
-  // Target byte addressed by a cell_row() value (0: the row before pkp -- garbage, never used).
+  // Target byte of the point whose cell_row() value is cv (0: the row before pkp -- garbage,
+  // never used).
   __device__ __forceinline__ uint32_t pkp_offset() const {
     return (uint32_t)(reinterpret_cast<const char*>(&pkp[0][0]) - reinterpret_cast<const char*>(this));
   }
   __device__ __forceinline__ const uint8_t* row_byte(uint32_t cv, int tid) const {
-    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv + 2 * tid;
+    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
   }
   __device__ __forceinline__ uint8_t* row_byte(uint32_t cv, int tid) {
-    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv + 2 * tid;
+    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
   }
-  // delivery cell of a target byte (target + 1; 0 reads the word before the table: never used)
+  // Delivery cell of a target byte (target + 1; 0 reads the word before the table: never used) in
+  // agent-word form: x << 8 | y << 24 in the target bytes, ones in the position bytes, so a pickup
+  // is one AND of the (idle: 0xFF target bytes) agent word.
   __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const { return tbl[C::T.dst / 4 - 1 + tb]; }
 };
 
@@ -780,15 +781,18 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     // points are cleared only after every agent's target byte has been read (clr[i]: the byte to
     // zero, row P = scratch).  The ascending move loop decides each agent three turns after its
     // move, when its lookups have landed, so only a few agents' lookups are live at a time.
-    uint64_t picked = 0;
+    uint32_t prlo = 0, prhi = 0;   // points picked up, rotated left by one (see pick)
     uint32_t clr[C::NAM];
     auto pick = [&](int i, uint32_t cpv, uint32_t tbv, uint32_t dstv) {
       const uint32_t a = s.ag[i];
       const uint32_t idle01 = (a >> 15) & 1u;   // delivery-target byte 0xFF
       const uint32_t m = 0u - __builtin_elementwise_min(__builtin_elementwise_min(cpv, tbv), idle01);
-      s.ag[i] = a ^ bop3<TA & (TB ^ TC)>(m, dstv << 8, IDLE);   // idle target bytes are 0xFF
-      picked |= (uint64_t)bop3<TA & TB>(m, 1u, 0u) << ((cpv / ROWB - 1u) & 63u);
-      clr[i] = msel(m, cpv, (uint32_t)(C::P + 1) * ROWB);
+      s.ag[i] = bop3<(TA & TB & TC) | (~TA & TB)>(m, a, dstv);   // idle target bytes are 0xFF
+      // bit (j + 1) mod 64 for point j (cpv = j + 1): rotated back once after the loop
+      const uint64_t bit = 1ull << (cpv & 63u);
+      prlo = bop3<(TA & TB) | TC>(m, (uint32_t)bit, prlo);
+      prhi = bop3<(TA & TB) | TC>(m, (uint32_t)(bit >> 32), prhi);
+      clr[i] = msel(m, cpv, (uint32_t)(C::P + 1));
       rewm[i] = m;
     };
 #ifndef WH_NO_PICK_IN_LOOP   // (A/B builds: -DWH_NO_PICK_IN_LOOP decides after the move loop)
@@ -1059,7 +1063,8 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       }
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) *L.row_byte(clr[i], tid) = 0;
-      s.am &= ~picked;
+      const uint64_t pr = ((uint64_t)prhi << 32) | prlo;
+      s.am &= ~((pr >> 1) | (pr << 63));
     }
   }
 
@@ -1469,10 +1474,27 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
   }
 }
 
+// -DWH_TIMING builds (tools/launch_timeline.py): per-wave s_memrealtime stamps (100 MHz) of the fused
+// rollout's phases -- entry, tables in LDS, state loaded, step loop done, state stored -- read back
+// with wh_debug_times.  Written by lane 0 of each wave with vector stores.
+#ifdef WH_TIMING
+constexpr int kTimeSlots = 6, kTimeWaves = 4096;
+__device__ unsigned long long g_wh_times[kTimeWaves * kTimeSlots];
+#define WH_T(i)                                                                                   \
+  do {                                                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                             \
+    const int w_ = (int)blockIdx.x * (BT / 64) + (int)(threadIdx.x >> 6);                        \
+    if ((threadIdx.x & 63) == 0 && w_ < kTimeWaves) g_wh_times[w_ * kTimeSlots + (i)] = now_;     \
+  } while (0)
+#else
+#define WH_T(i) ((void)0)
+#endif
+
 template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
   const int tid = threadIdx.x;
+  if (FAST) WH_T(0);
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
   const bool live = e < a.B && (FAST || !a.mask || a.mask[e]);
   const int na = FAST ? C::NAM : a.na;   // the fast instance runs na == NAM only (resolve_step)
@@ -1480,6 +1502,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   if (live) load_env_issue<C>(raw, a.state, a.B, e, na);
   load_tables<C>(L.tbl, a.tables);
   __syncthreads();
+  if (FAST) WH_T(1);
   if (!live) return;
   const Keys k{a.k0, a.k1};
   const uint32_t gid = (uint32_t)(a.env_offset + e);
@@ -1495,6 +1518,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
 #pragma unroll
   for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
+  if (FAST) WH_T(2);
 
   if (!FAST && a.phase == PH_POLICY) {
     uint32_t d[C::NAM];
@@ -1512,7 +1536,14 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
+  if (FAST) WH_T(3);
   store_env<C>(s, L, a.state, a.B, e, na, tid);
+#ifdef WH_TIMING
+  if (FAST) {
+    __builtin_amdgcn_s_waitcnt(0);   // the state stores have left the wave
+    WH_T(4);
+  }
+#endif
 }
 
 struct ResetParams {
@@ -1585,7 +1616,7 @@ struct ObsLds {
   uint32_t ptw[OBS_EB][C::PW];   // pickup target words (nonzero byte = active slot)
   uint32_t src[2][SRCW];
   uint32_t rp[C::P];             // pickup cell, x | y << 16
-  uint32_t dst[C::DP];           // delivery cell, x | y << 16
+  uint32_t dst[C::DP];           // delivery cell, x << 8 | y << 24 | 0x00FF00FF
 };
 
 // xfrag (optional): the same rows as the policy network's layer-0 B operand (policy_mlp.hip),
@@ -1650,11 +1681,11 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
         const uint32_t tg = (pt >> (8 * b)) & 0xFFu;
         if (tg && r < (uint32_t)R) {
           const uint32_t pxy = O.rp[4 * w + b];
-          const uint32_t dxy = O.dst[(tg - 1u) % C::DP];
+          const uint32_t dxy = O.dst[(tg - 1u) % C::DP];   // x << 8 | y << 24 (| 0x00FF00FF)
           im[Q0 + 4 * r] = (uint8_t)(pxy & 0xFFu);
           im[Q0 + 4 * r + 1] = (uint8_t)(pxy >> 16);
-          im[Q0 + 4 * r + 2] = (uint8_t)(dxy & 0xFFu);
-          im[Q0 + 4 * r + 3] = (uint8_t)(dxy >> 16);
+          im[Q0 + 4 * r + 2] = (uint8_t)(dxy >> 8);
+          im[Q0 + 4 * r + 3] = (uint8_t)(dxy >> 24);
           ++r;
         }
       }
@@ -1854,19 +1885,19 @@ int validate(const wh_config* c, Geometry* g) {
 }
 
 // Host copy of the per-workgroup tables, same layout as TableLayout (core.py:170-199):
-//   cell  [256*D] u16: (x | y << 8) -> (pickup index + 1) * ROWB, 0 = not a pickup cell
+//   cell  [256*D] u8 : (x | y << 8) -> pickup index + 1, 0 = not a pickup cell
 //   rp/tag [P+1] u32 pairs, interleaved (the policy reads both with one 8-byte LDS read):
 //          rp  = pickup cell as x | y << 16; [P] = far-away cell (never nearest)
 //          tag = pickup << 10 | x << 5 | y   (greedy argmin tag, solvers.py:53-58);
 //                [P] = the null cell (D/2, D/2): where fresh-reset agents head (core.py:233-236)
-//   dst   [Dp]   u32 : delivery cell as x | y << 16
+//   dst   [Dp]   u32 : delivery cell in agent-word target bytes, x << 8 | y << 24 | 0x00FF00FF
 //   mv    [12]   u32 : MOVES[a] as packed i16 (dx, dy) (core.py:38)
 //   valid [NV]   u32 : interior non-pickup cells x | y << 16, ascending (x, y) (spawn, core.py:191-199)
 std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   const int D = g.D;
   *bad = 0;
   if (D > 32) { *bad = 1; return {}; }
-  std::vector<uint16_t> cell(256 * D, 0);
+  std::vector<uint8_t> cell(256 * D, 0);
   std::vector<uint32_t> rp(g.P + 1), tag(g.P + 1);
   rp[g.P] = 0x00FF00FFu;
   tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);   // pickup << 10 | y << 5 | x
@@ -1877,7 +1908,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
         const int ci = x | (y << 8);
         if (cell[ci]) *bad = 1;  // overlapping racks
-        cell[ci] = (uint16_t)((j + 1) * ROWB);
+        cell[ci] = (uint8_t)(j + 1);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
         tag[j] = ((uint32_t)j << 10) | ((uint32_t)y << 5) | (uint32_t)x;
       }
@@ -1886,7 +1917,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
     const int v = 2 + d / 4, side = d % 4;
     const int x = (side & 1) ? (side == 3 ? D - 1 : 0) : v;
     const int y = (side & 1) ? v : (side == 2 ? D - 1 : 0);
-    dst[d] = (uint32_t)x | ((uint32_t)y << 16);
+    dst[d] = ((uint32_t)x << 8) | ((uint32_t)y << 24) | XY16;
   }
   std::vector<uint32_t> mv(12, 0);
   for (int a = 0; a < 9; ++a) {
@@ -1897,8 +1928,8 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   for (int x = 1; x < D - 1; ++x)
     for (int y = 1; y < D - 1; ++y)
       if (!cell[x | (y << 8)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
-  std::vector<uint32_t> words(cell.size() / 2, 0);
-  memcpy(words.data(), cell.data(), cell.size() * 2);
+  std::vector<uint32_t> words(cell.size() / 4, 0);
+  memcpy(words.data(), cell.data(), cell.size());
   for (int j = 0; j <= g.P; ++j) {
     words.push_back(rp[j]);
     words.push_back(tag[j]);
@@ -2031,6 +2062,15 @@ inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + BT - 1) / BT)); }
 
 // =============================================================================== C ABI
 extern "C" {
+
+#ifdef WH_TIMING
+int wh_debug_times(uint64_t* out, int32_t n) {   // timing builds only (not in the header)
+  if (!out || n < 0 || n > kTimeWaves * kTimeSlots) return WH_EINVAL;
+  hipError_t he = hipDeviceSynchronize();
+  if (he == hipSuccess) he = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wh_times), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+  return he == hipSuccess ? WH_OK : hip_err(he);
+}
+#endif
 
 int wh_check_read(uint64_t* out, int32_t clear) {
 #ifdef WH_CHECK
