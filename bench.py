@@ -344,6 +344,38 @@ def measure_sampler(env, K, W, dev, world, dist):
     return elapsed, split
 
 
+def measure_sampler_pipeline(env, K, W, dev, world, dist):
+    """The same sampler route as a two-stream pipeline (warehouse.vector.SamplerPipeline): step s + 1
+    (wh_sampler_step_to, double-buffered state) on the launch stream while the observation rows of
+    step s are written on a side stream -- the same launches and results as measure_sampler's.
+    hipGraph of G (even) steps.  Returns elapsed_s."""
+    import torch
+
+    from warehouse.vector import SamplerPipeline
+
+    pipe = SamplerPipeline(env, "greedy", 0.0)
+    pipe.begin()
+    for _ in range(max(W, 4)):
+        pipe.step()
+    pipe.end()
+    torch.cuda.synchronize(dev)
+    G = 100 if K >= 100 else max(2, K - K % 2)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        pipe.begin()
+        for _ in range(G):
+            pipe.step()
+        pipe.end()
+    torch.cuda.synchronize(dev)
+    reps = max(1, K // G)
+
+    def run():
+        for _ in range(reps):
+            graph.replay()
+
+    return timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist), reps * G
+
+
 def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     """scripts/rollout.py's loop on the device: per step the SAC policy network
     (wh_mlp_forward, argmax) over all B x NA observation rows, then wh_vector_step (step +
@@ -513,6 +545,7 @@ def main():
         el3, split = measure_sampler(env, Ks, W, dev, world, dist)
         oms = split["k_observe"]
         obs_b = B * NA * env.obs_len * 4 + B * 4 * words     # rows written + packed state read
+        el5, Kpp = measure_sampler_pipeline(env, Ks, W, dev, world, dist)
         sampler = {
             "workload": f"RLlib sampler route: device greedy policy fused with step + auto-reset (one 1-step "
                         f"wh_rollout launch), then f32 observation rows [B,{NA},{env.obs_len}] (wh_observe); "
@@ -520,6 +553,11 @@ def main():
             "value": aggregate_rate(world, B, NA, Ks, el3), "unit": "agent-steps/s", "steps": Ks,
             "ms_per_step": el3 * 1e3 / Ks,
             "kernel_split_ms": dict(split, rest=el3 * 1e3 / Ks - sum(split.values())),
+            "two_stream_pipeline": {
+                "workload": "the same launches as SamplerPipeline: the rows of step s on a side stream while "
+                            "step s+1 runs (state double-buffered); slower -- the step launch's workgroups only "
+                            "start as the observation kernel's drain (DESIGN.md §5)",
+                "value": aggregate_rate(world, B, NA, Kpp, el5), "steps": Kpp, "ms_per_step": el5 * 1e3 / Kpp},
             "roofline": {"bound": "hbm", "kernel": "k_observe", "kernel_ms": oms,
                          "bytes_per_launch": obs_b, "achieved": obs_b / (oms * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -190,6 +190,15 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
                     float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats,
                     int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
 
+/* wh_sampler_step's step launch with the state double-buffered and no observation rows: reads
+ * state_in, writes the stepped state to state_out (a distinct [words, B] buffer, or state_in itself).
+ * With two state buffers, wh_observe of step s (reading its output buffer) can run on another stream
+ * while step s + 1 reads the same buffer and writes the other one (warehouse/vector.py
+ * SamplerPipeline); the results are those of wh_sampler_step. */
+int wh_sampler_step_to(const wh_config* cfg, int64_t B, const uint32_t* state_in, uint32_t* state_out,
+                       int32_t policy, float p, float* rewards, uint8_t* dones, const wh_episode_stats* stats,
+                       int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
+
 /* A prepared wh_rollout: the same arguments resolved once (config validated, kernel and tables
  * chosen) into an opaque handle, so a loop that launches the same rollout repeatedly pays one
  * cheap call per launch (wh_launch_run enqueues exactly what wh_rollout would).  The buffers must

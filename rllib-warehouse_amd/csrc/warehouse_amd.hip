@@ -512,14 +512,17 @@ __device__ __forceinline__ void reset_lane(Regs<C>& s, Lds<C>& L, const Keys& k,
   const uint4 mine = stream_block(k, gid_l, ep, 0u, PUR_RESET, (uint32_t)(lane < NB ? lane : 0));
   auto word = [&](int j) -> uint32_t { return __builtin_amdgcn_readlane(comp(mine, j & 3), j >> 2); };
   const uint32_t n = variable_n ? 1u + __umulhi(word(0), (uint32_t)NA) : (uint32_t)NA;
+  // every spawn cell is read (all reads in flight together) and slots >= n are then masked: with
+  // `i < n` as the condition of the read, n being wave-uniform, each read sat in its own scalar
+  // branch behind a waitcnt -- NA serial LDS round trips per reset
+  uint32_t cell[C::NAM];
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i)
+    cell[i] = i < NA ? L.valid_cell(__umulhi(word(1 + i), (uint32_t)C::NV)) : 0u;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i) {
-    uint32_t a = IDLE;
-    if (i < NA) {
-      const uint32_t v = __umulhi(word(1 + i), (uint32_t)C::NV);
-      a = (i < (int)n) ? (L.valid_cell(v) | IDLE) : IDLE;
-    }
-    s.ag[i] = msel(me, a, s.ag[i]);
+    const uint32_t live = sgn((uint32_t)i - n);   // all-ones: i < n
+    s.ag[i] = msel(me, bop3<(TA & TB) | TC>(live, cell[i], IDLE), s.ag[i]);
   }
   if (lane < C::P) L.pkp[lane][col] = 0;
   if (lane < C::D) L.occ[lane][col] = 0u;
@@ -533,8 +536,12 @@ __device__ __forceinline__ void reset_lane(Regs<C>& s, Lds<C>& L, const Keys& k,
     const uint32_t r = __umulhi(word(1 + NA + 2 * j), m + 1u);
     const uint32_t sel = (j > 0 && ((S >> r) & 1ull)) ? m : r;
     S |= 1ull << sel;
-    selv = lane == j ? sel : selv;
-    tgv = lane == j ? __umulhi(word(2 + NA + 2 * j), (uint32_t)(C::DP - j)) : tgv;   // rank r2_j
+    // (computed on every lane, then selected: as `lane == j ? rank : tgv` each item was an
+    // exec-masked branch, ~8 issue slots of branching per item)
+    const uint32_t rank = __umulhi(word(2 + NA + 2 * j), (uint32_t)(C::DP - j));   // r2_j
+    const uint32_t mj = mask_z((uint32_t)(lane ^ j));
+    selv = msel(mj, sel, selv);
+    tgv = msel(mj, rank, tgv);
   }
   // targets: item j is the r2_j-th delivery point not taken by items < j.  Decoded in parallel
   // (lane j holds item j): from the last item back, every later item at or above item j's value
@@ -1305,6 +1312,8 @@ struct StepParams {
   int32_t ablate;  // timing-only phase skips (env WH_ABLATE), never set in normal use
   wh_episode_stats stats;   // all-NULL = off
   const uint8_t* mask;      // [B] or NULL: envs to step (wh_vector_step)
+  uint32_t* state_out;      // NULL: in place; else the state is read from `state`, written here
+                            // (wh_sampler_step_to: double-buffered, no mask)
 };
 
 // Folds the episodes this wave finished into the per-n bins of wh_episode_stats (the
@@ -1537,7 +1546,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
   if (FAST) WH_T(3);
-  store_env<C>(s, L, a.state, a.B, e, na, tid);
+  store_env<C>(s, L, a.state_out ? a.state_out : a.state, a.B, e, na, tid);
 #ifdef WH_TIMING
   if (FAST) {
     __builtin_amdgcn_s_waitcnt(0);   // the state stores have left the wave
@@ -2428,6 +2437,28 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
   int rc = launch_step(cfg, B, state, policy, a, stream);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
+}
+
+int wh_sampler_step_to(const wh_config* cfg, int64_t B, const uint32_t* state_in, uint32_t* state_out,
+                       int32_t policy, float p, float* rewards, uint8_t* dones, const wh_episode_stats* stats,
+                       int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream) {
+  if (policy != WH_POLICY_GREEDY && policy != WH_POLICY_RANDOM) return WH_EINVAL;
+  if (!(p >= 0.0f && p <= 1.0f) || !stats_ok(stats)) return WH_EINVAL;
+  if (B > 0 && !state_out) return WH_EINVAL;
+  StepParams a{};
+  if (stats) a.stats = *stats;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.p = p;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = 1;
+  a.phase = PH_ALL;
+  a.autoreset = 1;
+  a.variable_n = variable_n ? 1 : 0;
+  a.state_out = state_out;   // every env is live (no mask): each lane stores its whole state
+  return launch_step(cfg, B, const_cast<uint32_t*>(state_in), policy, a, stream);
 }
 
 }  // extern "C"

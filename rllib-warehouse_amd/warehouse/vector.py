@@ -224,3 +224,77 @@ class WarehouseBaseEnv:
 
     def custom_metrics(self) -> Dict[str, Dict[str, float]]:
         return self.vec.custom_metrics()
+
+
+class SamplerPipeline:
+    """The sampler route with the device policy (BatchedWarehouse.sampler_step) as a two-stream
+    pipeline: the observation rows of step s are written on a side stream while step s + 1 runs on
+    the current stream.  Both only READ the state step s produced, so the state is double-buffered
+    (wh_sampler_step_to reads one buffer and writes the other) and so are the outputs: step s
+    writes rewards[s % 2] / dones[s % 2], its rows land in obs[s % 2].  Step s + 2 writes the buffer
+    observe(s) reads, so it waits for that observe (an event); nothing else is ordered, so the step
+    kernel (one workgroup per CU) and the observation kernel (HBM-write bound) share the chip.
+    Results equal sampler_step's: the same launches on the same states (tests/test_gpu_vector.py).
+
+    step() returns (obs, rewards, dones) of that step; obs is complete once `ready(s)` has been
+    waited on (or after synchronize()); use it before step s + 2 reuses its buffer.  env.state
+    always names the newest state buffer.  Inside a CUDA-graph capture call begin() first and end()
+    last (the side stream forks from and joins the capturing stream)."""
+
+    def __init__(self, env: BatchedWarehouse, policy: str = "greedy", p: float = 0.0):
+        from . import _native as nat
+        from .batched import POLICIES
+
+        self.env, self.policy, self.p = env, POLICIES[policy], float(p)
+        self._nat = nat
+        dev = env.device
+        self.bufs = [env.state, torch.empty_like(env.state)]
+        shape = (env.B, env.agent_slots, env.obs_len)
+        self.obs = [torch.empty(shape, dtype=torch.float32, device=dev) for _ in range(2)]
+        self.rewards = [torch.zeros((env.B, env.agent_slots), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.dones = [torch.zeros(env.B, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.side = torch.cuda.Stream(device=dev)
+        self.step_ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.obs_ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.pending = [False, False]   # obs_ev[k] recorded and not yet waited on by the main stream
+        self.s = 0
+        self.cur = 0                    # bufs[cur] holds the newest state
+
+    def begin(self) -> None:
+        """Fork the side stream from the current stream (start of a capture / after a sync)."""
+        self.side.wait_stream(torch.cuda.current_stream(self.env.device))
+        self.pending = [False, False]
+
+    def end(self) -> None:
+        """Join: the current stream waits for every observation launched so far."""
+        torch.cuda.current_stream(self.env.device).wait_stream(self.side)
+        self.pending = [False, False]
+
+    def step(self):
+        env, nat = self.env, self._nat
+        i, o = self.cur, 1 - self.cur
+        k = self.s % 2
+        main = torch.cuda.current_stream(env.device)
+        if self.pending[k]:              # observe(s - 2) read bufs[o]: let it finish first
+            main.wait_event(self.obs_ev[k])
+            self.pending[k] = False
+        nat.check(nat.lib().wh_sampler_step_to(
+            env._cfgp, env.B, self.bufs[i].data_ptr(), self.bufs[o].data_ptr(), self.policy, self.p,
+            self.rewards[k].data_ptr(), self.dones[k].data_ptr(),
+            None if env.stats is None else env.stats.ref, int(env.train), env.seed, env.env_offset,
+            nat.stream_of(env.device)), "wh_sampler_step_to")
+        self.step_ev[k].record(main)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.step_ev[k])
+            nat.check(nat.lib().wh_observe(env._cfgp, env.B, self.bufs[o].data_ptr(), self.obs[k].data_ptr(),
+                                           nat.stream_of(env.device)), "wh_observe")
+            self.obs_ev[k].record(self.side)
+        self.pending[k] = True
+        self.cur = o
+        env.state = self.bufs[o]
+        self.s += 1
+        return self.obs[k], self.rewards[k], self.dones[k]
+
+    def ready(self, s: int) -> torch.cuda.Event:
+        """Event after which step s's observation rows are written (valid until step s + 2)."""
+        return self.obs_ev[s % 2]

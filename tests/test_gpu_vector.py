@@ -452,3 +452,53 @@ def test_sampler_observation_rows_equal_wh_observe(wh, variant, na, train, B):
         fused = obs.clone()
         ref = env.observe()
         assert torch.equal(fused, ref), f"step {s}"
+
+
+
+@pytest.mark.parametrize("variant,na,train,p,graph", [("medium", 8, False, 0.0, False), ("medium", 9, True, 0.2, False),
+                                                      ("large", 16, False, 0.0, True), ("small", 4, True, 0.1, True)])
+def test_sampler_pipeline_equals_sampler_step(wh, variant, na, train, p, graph):
+    """SamplerPipeline (wh_sampler_step_to into the other state buffer on the current stream, the
+    observation rows of step s on a side stream while step s + 1 runs) == sampler_step step by
+    step: rewards, dones, observation rows, episode metrics and the final state over 216 steps
+    (an episode end), eagerly and as a captured CUDA graph of 4-step blocks (the bench's form: an
+    even block, so every replay starts from the same state buffer)."""
+    import torch
+
+    from warehouse.vector import SamplerPipeline
+
+    B, seed, K, G = 2048 + 77, 5, 216, 4
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    sa, sb = a.enable_episode_stats(), b.enable_episode_stats()
+    a.reset()
+    b.reset()
+    pipe = SamplerPipeline(a, "greedy", p)
+    dev = a.device
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(g):   # capture launches nothing: replays start from the reset state
+            pipe.begin()
+            outs = [pipe.step() for _ in range(G)]
+            pipe.end()
+        torch.cuda.synchronize(dev)
+    s = 0
+    while s < K:
+        if graph:
+            g.replay()
+            got = outs
+        else:
+            got = [pipe.step()]
+        torch.cuda.synchronize(dev)
+        for j, (oa, ra, da) in enumerate(got):
+            ob_, rb, db = b.sampler_step("greedy", p)
+            s += 1
+            if j < len(got) - 2:   # its buffers were reused by step j + 2 of the block
+                continue
+            assert torch.equal(ra, rb), f"rewards step {s}"
+            assert torch.equal(da, db), f"dones step {s}"
+            assert torch.equal(oa, ob_), f"obs step {s}"
+    assert torch.equal(a.state, b.state)   # (every step's rewards also enter the episode metrics)
+    for k in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
+        assert torch.equal(getattr(sa, k), getattr(sb, k)), k

@@ -18,7 +18,7 @@ for s in "$@"; do
   i=$((i+1))
   case "$s" in
     smoke)  step smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    pytest) step pytest 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench)  step bench 600 python bench.py ;;
     *)      step custom$i 900 bash -c "$s" ;;
   esac
