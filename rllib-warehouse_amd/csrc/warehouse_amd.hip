@@ -274,6 +274,13 @@ struct Lds {
   // Agent words when processing in action-dict order; afterwards the reward-row staging area.
   // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
   alignas(16) uint32_t agl[C::NAM][BT];
+  // Reset slots (fused rollout): lane tid's NEXT episode's reset state, precomputed for the whole
+  // wave at once (reset_philox<..., TO_SLOT>) and consumed when the lane ends its episode
+  // (reset_from_slot): agent words, R requests (point | (target + 1) << 8), open mask, header, and
+  // the episode the slot was computed for (valid iff rs_ep == epi + 1).
+  uint32_t rs_ag[C::NAM][BT];
+  uint16_t rs_req[C::R][BT];
+  uint32_t rs_am[2][BT], rs_hdr[BT], rs_ep[BT];
   // Cell (x | y << 16) -> pickup index + 1, 0 for other cells: one v_perm (the byte index
   // x | y << 8) + one ds_read_u8; the point's row in pkp is then one v_lshl_add away (row_byte).
   __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
@@ -428,7 +435,9 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 // them with the points in Floyd's order is a uniform injection.  NAC >= 0 is the agent count at
 // compile time (the fused rollout): every stream word then has a fixed place in the precomputed
 // Philox blocks, and the whole reset is straight-line code.
-template <class C, int NAC = -1>
+// TO_SLOT: the same draws and results for every lane, written to the lane's reset slot (Lds::rs_*)
+// instead of its registers and pickup plane, for episode epi + 1.
+template <class C, int NAC = -1, bool TO_SLOT = false>
 __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
                                              int na_rt, int variable_n, uint32_t W, int tid) {
   WH_PHASE_MARK(reset);
@@ -454,10 +463,13 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
       const uint32_t cell = L.valid_cell(v);
       a = (i < (int)n) ? (cell | IDLE) : IDLE;
     }
-    s.ag[i] = a;
+    if (TO_SLOT) L.rs_ag[i][tid] = a;
+    else s.ag[i] = a;
   }
+  if (!TO_SLOT) {
 #pragma unroll
-  for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+    for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+  }
   const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
   uint32_t plo = 0, phi = 0;                // Floyd's subset so far
   uint32_t sel[C::R], tg[C::R];
@@ -483,12 +495,46 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
   for (int j = C::R - 2; j >= 0; --j)
 #pragma unroll
     for (int i = j + 1; i < C::R; ++i) tg[i] += 1u - ((tg[i] - tg[j]) >> 31);   // + (tg[i] >= tg[j])
+  if (TO_SLOT) {
 #pragma unroll
-  for (int j = 0; j < C::R; ++j) L.pkp[sel[j]][tid] = (uint16_t)((tg[j] + 1u) | wexp);
-  s.am = ((uint64_t)phi << 32) | plo;
-  s.hdr = (n << 16) | (1u << 24);
-  s.epi = ep;
+    for (int j = 0; j < C::R; ++j) L.rs_req[j][tid] = (uint16_t)(sel[j] | ((tg[j] + 1u) << 8));
+    L.rs_am[0][tid] = plo;
+    L.rs_am[1][tid] = phi;
+    L.rs_hdr[tid] = (n << 16) | (1u << 24);
+    L.rs_ep[tid] = ep;
+  } else {
+#pragma unroll
+    for (int j = 0; j < C::R; ++j) L.pkp[sel[j]][tid] = (uint16_t)((tg[j] + 1u) | wexp);
+    s.am = ((uint64_t)phi << 32) | plo;
+    s.hdr = (n << 16) | (1u << 24);
+    s.epi = ep;
+  }
   WH_PHASE_MARK(reset_end);
+}
+
+// The reset of the env of lane l of this wave from its reset slot (valid: rs_ep == epi + 1), by
+// the whole wave: agent words and request cells read across lanes (lane i reads field i of lane
+// l's column), the pickup-plane and occupancy columns cleared and written one cell per lane.
+// Bit-identical to reset_philox<C, NA> (plus the occupancy clear) for that env, for ~40 issue slots
+// instead of a Philox block per lane, a Floyd chain on wave-uniform values and the rank decode.
+template <class C, int NA>
+__device__ __forceinline__ void reset_from_slot(Regs<C>& s, Lds<C>& L, uint32_t W, int tid, int l) {
+  WH_PHASE_MARK(slot_reset);
+  const int lane = tid & 63;
+  const int col = (tid & ~63) + l;
+  const uint32_t me = mask_z((uint32_t)(lane ^ l));
+  const uint32_t av = L.rs_ag[lane < NA ? lane : 0][col];
+  const uint32_t rq = L.rs_req[lane < C::R ? lane : 0][col];
+  const uint32_t alo = L.rs_am[0][col], ahi = L.rs_am[1][col], hdr = L.rs_hdr[col];
+#pragma unroll
+  for (int i = 0; i < C::NAM; ++i)
+    s.ag[i] = msel(me, i < NA ? (uint32_t)__builtin_amdgcn_readlane(av, i) : IDLE, s.ag[i]);
+  if (lane < C::P) L.pkp[lane][col] = 0;
+  if (lane < C::D) L.occ[lane][col] = 0u;
+  if (lane < C::R) L.pkp[rq & 0xFFu][col] = (uint16_t)((rq >> 8) | ((W & 0xFFu) << 8));   // after the clear
+  s.am = ((uint64_t)msel(me, ahi, (uint32_t)(s.am >> 32)) << 32) | msel(me, alo, (uint32_t)s.am);
+  s.hdr = msel(me, hdr, s.hdr);
+  s.epi = msel(me, s.epi + 1u, s.epi);
 }
 
 // The same philox reset for ONE env -- the env of lane l of this wave -- computed by the whole
@@ -1470,7 +1516,16 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
 #else
       if (false) {
 #endif
+#ifndef WH_NO_RESET_SLOTS   // (A/B builds: -DWH_NO_RESET_SLOTS resets the lane from scratch)
+        // its precomputed next-episode state, after (re)filling the wave's slots if this lane's is
+        // stale: one wave-wide fill (every lane's next episode) serves the resets of the lanes
+        // that end later in this launch
+        if (__any(done && L.rs_ep[tid] != s.epi + 1u))
+          reset_philox<C, C::NAM, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+        reset_from_slot<C, C::NAM>(s, L, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+#else
         reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+#endif
         lg.rebuild = lg.rebuild || done;   // its grid column was cleared
       } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
@@ -1527,6 +1582,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
 #pragma unroll
   for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
+  if (FAST) L.rs_ep[tid] = s.epi;                       // reset slots start stale (!= epi + 1)
   if (FAST) WH_T(2);
 
   if (!FAST && a.phase == PH_POLICY) {
