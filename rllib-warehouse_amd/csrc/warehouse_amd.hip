@@ -1466,6 +1466,13 @@ constexpr bool kLazyGrid = true;
 constexpr bool kLazyGrid = false;
 #endif
 
+// Lanes of a wave ending their episodes in the same step that are reset one at a time from their
+// reset slots (~40 issue slots each); more than this take the all-lane reset_philox (~700 VALU).
+constexpr int kSlotResetMax = 8;
+// A fill costs about two single-lane resets and a launch of K desynchronised steps ends ~K/3 episodes
+// per wave (Medium-8), so launches shorter than this reset single lanes from scratch (reset_lane).
+constexpr int kSlotMinSteps = 8;
+
 template <class C>
 __device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]) {
   if constexpr ((C::NAM & 3) == 0) {
@@ -1509,23 +1516,23 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
     drow += a.B;
     if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
       const uint64_t dm = __ballot(done);
-      // one env of a full wave ends (desynchronised episodes): a wave-wide reset of it (every lane
-      // takes part, so not in a tail wave whose lanes past B have exited)
-#ifndef WH_NO_LANE_RESET   // (A/B builds: tools/build_variant.sh nolane -DWH_NO_LANE_RESET)
-      if (__popcll(dm) == 1 && __ballot(true) == ~0ull) {
-#else
-      if (false) {
-#endif
-#ifndef WH_NO_RESET_SLOTS   // (A/B builds: -DWH_NO_RESET_SLOTS resets the lane from scratch)
-        // its precomputed next-episode state, after (re)filling the wave's slots if this lane's is
-        // stale: one wave-wide fill (every lane's next episode) serves the resets of the lanes
-        // that end later in this launch
+      // a few envs of a full wave end (desynchronised episodes): wave-wide resets of them, one env
+      // at a time (every lane takes part, so not in a tail wave whose lanes past B have exited)
+      const bool full = __ballot(true) == ~0ull;
+#ifndef WH_NO_RESET_SLOTS   // (A/B builds: -DWH_NO_RESET_SLOTS resets one lane from scratch)
+      if (a.steps >= kSlotMinSteps && __popcll(dm) <= kSlotResetMax && full) {
+        // their precomputed next-episode states, after (re)filling the wave's slots if one of
+        // theirs is stale: one wave-wide fill (every lane's next episode) serves the resets of
+        // the lanes that end later in this launch
         if (__any(done && L.rs_ep[tid] != s.epi + 1u))
           reset_philox<C, C::NAM, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
-        reset_from_slot<C, C::NAM>(s, L, (uint32_t)a.W, tid, __builtin_ctzll(dm));
-#else
-        reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+        for (uint64_t m = dm; m; m &= m - 1ull) reset_from_slot<C, C::NAM>(s, L, (uint32_t)a.W, tid, __builtin_ctzll(m));
+        lg.rebuild = lg.rebuild || done;   // their grid columns were cleared
+      } else
 #endif
+      if (__popcll(dm) == 1 && full) {
+        // short launches (the sampler's 1-step ones): a fill would serve few later resets
+        reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
         lg.rebuild = lg.rebuild || done;   // its grid column was cleared
       } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
