@@ -43,6 +43,11 @@ METRIC = "agent-steps/sec (aggregate) at B=65536 envs × 8 agents, 1/2/4/8 MI355
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters (spec)
 MFMA_BF16_PEAK_TFS = 2500.0   # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 MFMA_F32_PEAK_TFS = 157.3     # f32-input MFMA peak (= the f32 vector rate), MI355X_MICROARCH.md
+# VALU issue peak of the chip: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles
+# at the 2.4 GHz max clock (MI355X_MICROARCH.md, execution model: a wave issues each VALU over 2
+# cycles; one wave ALONE sustains one per 4, so a one-wave-per-SIMD kernel tops out at half of this)
+SIMDS = 256 * 4
+VALU_PEAK_GIPS = SIMDS * 2.4 / 2   # G wave-instructions/s
 
 
 def cpu_worker(args):
@@ -107,17 +112,13 @@ def cpu_baseline(variant, n, procs, seconds, detail=""):
 
 
 def source_sha():
-    """sha256 of the kernel sources (csrc/*.hip + *.h, sorted; the hash the Makefile bakes into
-    wh_version()): profile-derived fields are reported only when the committed profile was taken
-    from the same sources, and the run refuses a library built from other sources."""
-    import hashlib
+    """The tree's source sha (warehouse/_native.py:tree_source_sha: csrc/*.hip, *.h, *.cpp, the
+    Makefile and include/warehouse_amd.h -- the hash the Makefile bakes into wh_version()):
+    profile-derived fields are reported only when the committed profile was taken from the same
+    sources, and the run refuses a library built from other sources or settings."""
+    from warehouse import _native
 
-    h = hashlib.sha256()
-    csrc = os.path.join(ROOT, "rllib-warehouse_amd", "csrc")
-    for f in sorted(os.listdir(csrc)):
-        if f.endswith((".hip", ".h")):
-            h.update(open(os.path.join(csrc, f), "rb").read())
-    return h.hexdigest()[:16]
+    return _native.tree_source_sha()
 
 
 def load_profile(tag):
@@ -143,8 +144,10 @@ def config_name(variant, na, envs, policy):
 
 def load_issue(tag, steps_per_launch):
     """VALU issue view of the step kernel from the committed SQ counters (profiles/pmc_traffic.json,
-    same kernel sources only): per wave and env-step, VALU instructions and wave quad-cycles; one
-    wave alone issues at most one VALU per quad-cycle (MI355X_MICROARCH.md)."""
+    same kernel sources only): per wave and env-step, VALU instructions and wave quad-cycles.
+    `single_wave_issue_occupancy` = VALU per wave quad-cycle: the share of the issue slots ONE wave
+    can use (one VALU per 4 cycles) that it fills -- an occupancy, not a roofline fraction (two waves
+    per SIMD could issue twice as many; the chip-level fraction is roofline.valu)."""
     d = load_profile(tag)
     try:
         sq = d["sq"]
@@ -152,11 +155,30 @@ def load_issue(tag, steps_per_launch):
         waves = sq["SQ_WAVES"]
         valu = sq["SQ_INSTS_VALU"] / waves / spl
         cyc = sq["SQ_WAVE_CYCLES"] / waves / spl
-        return {"valu_per_wave_step": valu, "wave_quad_cycles_per_step": cyc, "valu_issue_frac": valu / cyc,
+        return {"valu_per_wave_step": valu, "wave_quad_cycles_per_step": cyc,
+                "single_wave_issue_occupancy": valu / cyc,
+                "wait_quad_cycles_per_step": sq.get("SQ_WAIT_ANY", 0.0) / waves / spl,
                 "lds_per_wave_step": sq["SQ_INSTS_LDS"] / waves / spl,
                 "source": f"profiles/pmc_traffic.json:{tag}.sq ({spl} steps per launch)"}
     except Exception:
         return None
+
+
+def valu_roofline(prof, kernel_ms):
+    """The chip-level VALU roofline of a kernel: SQ_INSTS_VALU per launch (same-sha SQ profile) / the
+    launch's duration / VALU_PEAK_GIPS.  `frac` uses the live HIP-event duration of the timed launch,
+    `frac_rocprof` the profile's own kernel-trace average.  None without a same-sha SQ profile."""
+    try:
+        v = prof["sq"]["SQ_INSTS_VALU"]
+    except (TypeError, KeyError):
+        return None
+    out = {"valu_per_launch": v, "achieved": v / (kernel_ms * 1e-3) / 1e9, "peak": VALU_PEAK_GIPS,
+           "unit": "G wave64-VALU/s", "frac": v / (kernel_ms * 1e-3) / 1e9 / VALU_PEAK_GIPS,
+           "peak_basis": f"{SIMDS} SIMDs x 2.4 GHz / 2 cycles per wave64 VALU (MI355X_MICROARCH.md)"}
+    if prof.get("avg_ns"):
+        out["rocprof_avg_ms"] = prof["avg_ns"] * 1e-6
+        out["frac_rocprof"] = v / (prof["avg_ns"] * 1e-9) / 1e9 / VALU_PEAK_GIPS
+    return out
 
 
 # ----------------------------------------------------------------------------- multi-GPU plumbing
@@ -298,10 +320,11 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist, position=True):
 
 def measure_sampler(env, K, W, dev, world, dist):
     """The RLlib sampler route (scripts/train.py's workload): per step the device greedy policy
-    stands in for the learner's policy -- fused into the step launch (BatchedWarehouse.sampler_step:
-    one 1-step wh_rollout = policy + step + auto-reset, then wh_observe = observation rows
-    [B,NA,9R+1] f32).  hipGraph of G steps.  Returns (elapsed_s, {kernel: ms per launch}) with each
-    kernel timed alone between HIP events on the launch stream (20 back-to-back launches)."""
+    stands in for the learner's policy -- BatchedWarehouse.sampler_step = wh_sampler_step: policy +
+    step + auto-reset + observation rows [B,NA,9R+1] f32 in ONE launch (k_sampler).  hipGraph of G
+    steps.  Returns (elapsed_s, {kernel: ms per launch}) with each launch form timed alone between
+    HIP events on the launch stream (20 back-to-back launches): the fused launch, and for comparison
+    the two-launch form it replaces (the 1-step fused-rollout launch, then wh_observe)."""
     import torch
 
     stream = torch.cuda.current_stream(dev)
@@ -338,9 +361,10 @@ def measure_sampler(env, K, W, dev, world, dist):
         kms = sorted(a.elapsed_time(b) / 20 for a, b in evs)
         return kms[len(kms) // 2]
 
-    split = {"k_observe": per_launch(env.observe),
-             "k_step (1-step rollout: greedy + step + auto-reset)": per_launch(
-                 lambda: env.sampler_step("greedy", 0.0, observe=False))}
+    split = {"k_sampler (fused: greedy + step + auto-reset + rows)": per_launch(one),
+             "two-launch form: k_step (1-step rollout)": per_launch(
+                 lambda: env.sampler_step("greedy", 0.0, observe=False)),
+             "two-launch form: k_observe": per_launch(env.observe)}
     return elapsed, split
 
 
@@ -435,15 +459,25 @@ def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
 
 
 def step_roofline(m, variant, NA, policy, mode):
-    """The bench line's `roofline` for the timed launches of measure() (dict m)."""
+    """The bench line's `roofline` for the timed launches of measure() (dict m).  achieved / peak /
+    frac are the contract's HBM figures (algorithmic bytes per launch / the launch's event-timed
+    duration, against 8 TB/s); `valu` is the chip-level VALU issue roofline of the same launch (from
+    the same-sha SQ profile), and `bound` names whichever of the two fractions is higher -- the
+    step kernel keeps its state in registers and is VALU-issue bound."""
     tag = f"{variant}_n{NA}_{mode}_k{m['steps_per_launch']}"
     prof = load_profile(tag)
+    hbm_frac = m["achieved_gbs"] / HBM_PEAK_GBS
+    valu = valu_roofline(prof, m["kernel_ms"])
+    bound = "valu" if valu is not None and valu["frac"] > hbm_frac else "hbm"
     return {
-        "bound": "hbm",
+        "bound": bound,
         "achieved": m["achieved_gbs"],
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": m["achieved_gbs"] / HBM_PEAK_GBS,
+        "frac": hbm_frac,
+        "hbm_frac": hbm_frac,
+        "valu_frac": None if valu is None else valu["frac"],
+        "valu": valu,
         "traffic": None if prof is None else prof.get("bytes_per_launch"),
         "kernel": f"k_step<Cfg<D,R,racks,{NA}>, {policy}>",
         "kernel_ms": m["kernel_ms"],
@@ -455,12 +489,26 @@ def step_roofline(m, variant, NA, policy, mode):
         "rocprof_avg_ms": None if prof is None or prof.get("avg_ns") is None else prof["avg_ns"] * 1e-6,
         "issue": load_issue(tag, m["steps_per_launch"]),
         "profile": None if prof is None else f"profiles/pmc_traffic.json:{tag}",
-        "note": "kernel_ms = HIP-event span of the timed launches / launches (events on the launch "
-                "stream inside the timed window); host_fixed_us = window wall time - that span "
-                "(launch + completion latency); algorithmic bytes = 2 x packed state + per-step "
-                "rewards/dones; the kernel keeps state in registers and is VALU-issue bound "
-                "(DESIGN.md §5)",
+        "note": "achieved/peak/frac: HBM (algorithmic bytes = 2 x packed state + per-step rewards/dones, per "
+                "launch / kernel_ms); valu: SQ_INSTS_VALU of the same launch shape / kernel_ms against "
+                "1,024 SIMDs x 1.2 G wave64-VALU/s; bound = the larger fraction.  kernel_ms = HIP-event "
+                "span of the timed launches / launches (events on the launch stream inside the timed "
+                "window); host_fixed_us = window wall time - that span (launch + completion latency)",
     }
+
+
+def report(out, args):
+    """Rank 0's line: `out` plus the host-core baseline of the same workload (cpu_baseline: the numpy
+    restatement of Warehouse.step() on a bounded sample, one process per host core), timed after the
+    GPU window at EVERY world size, so a 1/2/4/8-GPU run carries the host-core figure of the same run.
+    Prints the JSON line and returns it."""
+    if not args.no_cpu_baseline:
+        cores, detail = host_cores()
+        procs = args.cpu_procs or cores
+        out["cpu_baseline"] = cpu_baseline(args.variant, args.agents, procs, args.cpu_seconds, detail)
+        out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    print(json.dumps(out), flush=True)
+    return out
 
 
 def main():
@@ -543,26 +591,29 @@ def main():
     if not args.no_sampler:
         Ks = min(K, 1000)
         el3, split = measure_sampler(env, Ks, W, dev, world, dist)
-        oms = split["k_observe"]
-        obs_b = B * NA * env.obs_len * 4 + B * 4 * words     # rows written + packed state read
+        fms = split["k_sampler (fused: greedy + step + auto-reset + rows)"]
+        # algorithmic bytes of the fused launch: rows written + packed state read and written +
+        # rewards + dones
+        samp_b = B * NA * env.obs_len * 4 + 2 * B * 4 * words + B * (4 * NA + 1)
         el5, Kpp = measure_sampler_pipeline(env, Ks, W, dev, world, dist)
         sampler = {
-            "workload": f"RLlib sampler route: device greedy policy fused with step + auto-reset (one 1-step "
-                        f"wh_rollout launch), then f32 observation rows [B,{NA},{env.obs_len}] (wh_observe); "
-                        f"hipGraph of 100 steps",
+            "workload": f"RLlib sampler route: device greedy policy + step + auto-reset + f32 observation rows "
+                        f"[B,{NA},{env.obs_len}] in one launch (wh_sampler_step -> k_sampler); hipGraph of 100 steps",
             "value": aggregate_rate(world, B, NA, Ks, el3), "unit": "agent-steps/s", "steps": Ks,
             "ms_per_step": el3 * 1e3 / Ks,
-            "kernel_split_ms": dict(split, rest=el3 * 1e3 / Ks - sum(split.values())),
+            "kernel_split_ms": split,
+            "two_launch_form_ms": split["two-launch form: k_step (1-step rollout)"] + split["two-launch form: k_observe"],
             "two_stream_pipeline": {
-                "workload": "the same launches as SamplerPipeline: the rows of step s on a side stream while "
+                "workload": "the two-launch form as SamplerPipeline: the rows of step s on a side stream while "
                             "step s+1 runs (state double-buffered); slower -- the step launch's workgroups only "
                             "start as the observation kernel's drain (DESIGN.md §5)",
                 "value": aggregate_rate(world, B, NA, Kpp, el5), "steps": Kpp, "ms_per_step": el5 * 1e3 / Kpp},
-            "roofline": {"bound": "hbm", "kernel": "k_observe", "kernel_ms": oms,
-                         "bytes_per_launch": obs_b, "achieved": obs_b / (oms * 1e-3) / 1e9,
+            "roofline": {"bound": "hbm", "kernel": "k_sampler", "kernel_ms": fms,
+                         "bytes_per_launch": samp_b, "achieved": samp_b / (fms * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": obs_b / (oms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": load_traffic(f"{args.variant}_n{NA}_observe")},
+                         "frac": samp_b / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": load_traffic(f"{args.variant}_n{NA}_sampler"),
+                         "note": "algorithmic bytes = B*NA*(9R+1)*4 rows + 2 x packed state + rewards + dones"},
         }
 
     policy_line = policy_f32 = None
@@ -628,12 +679,7 @@ def main():
             "policy_path": policy_line,
             "policy_path_f32": policy_f32,
         }
-        if not args.no_cpu_baseline and world == 1:   # reported at N=1 only
-            cores, detail = host_cores()
-            procs = args.cpu_procs or cores
-            out["cpu_baseline"] = cpu_baseline(args.variant, NA, procs, args.cpu_seconds, detail)
-            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-        print(json.dumps(out), flush=True)
+        report(out, args)
     if world > 1:
         dist.destroy_process_group()
 

@@ -108,7 +108,10 @@ int wh_reset(const wh_config* cfg, int64_t B, uint32_t* state, const uint8_t* ma
 /* Warehouse.step(action_dict)  (warehouse/core.py:262-442).
  *   actions   [B,NA] int32 in 0..8 (MOVES index, core.py:38; the host wraps -9..-1 like Python)
  *   order     [B,NA] int32 or NULL: action-dict iteration order (core.py:279), -1 terminated;
- *             agents not listed do not move.  NULL = ascending agent id.
+ *             agents not listed do not move.  NULL = ascending agent id.  Entry = agent id in
+ *             bits 0-7, optionally (bits 8-15) that dict entry's own action + 1, 0 = actions[e,id]:
+ *             a dict naming one agent under two keys ('0' and 0, or '-1' and str(n-1): int(key)
+ *             indexes like numpy, core.py:280) moves it once per entry with that entry's action.
  *   rewards   [B,NA] float32 (core.py:334-368), dones [B] uint8 (core.py:438); either may be NULL
  *   regen     [B,2R] int32 or NULL (philox): R positions into the ascending list of inactive
  *             pickups (the index np.random.choice(inactive,k) picked), then R delivery targets;
@@ -173,6 +176,7 @@ int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, 
  *   order   [B,NA] int32 or NULL: each env's action-dict iteration order (core.py:279), -1
  *           terminated; agents not listed are skipped -- they neither move nor re-mark their cell
  *           (core.py:279-300 only visits the dict's keys).  NULL = every agent, ascending id.
+ *           Entries as wh_step's (bits 8-15: the entry's own action + 1, for repeated agents).
  *   mask [B] uint8 or NULL: only envs with mask != 0 are stepped (the others keep their state;
  *   their rewards/dones are not written); rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats
  *   may be NULL. */

@@ -188,12 +188,16 @@ def step(L: Layout, S: BState, actions: np.ndarray, draws, order: Optional[np.nd
         if order is None:
             idx = np.full(B, s)
             act = s < S.n
+            a = acts[b, idx]
         else:
-            idx = np.asarray(order[:, s], np.int64)
-            act = idx >= 0
-            idx = np.maximum(idx, 0)
+            # entry = agent id (bits 0-7) | the entry's own action + 1 (bits 8-15, 0: actions[id]),
+            # -1 terminated (include/warehouse_amd.h, wh_step)
+            raw = np.asarray(order[:, s], np.int64)
+            act = raw >= 0
+            idx = np.where(act, raw & 0xFF, 0)
+            sact = np.where(act, (raw >> 8) & 0xFF, 0)
+            a = np.where(sact > 0, sact - 1, acts[b, idx])
         px, py = S.pos[b, idx, 0].astype(np.int64), S.pos[b, idx, 1].astype(np.int64)
-        a = acts[b, idx]
         x, y = px + a // 3 - 1, py + a % 3 - 1
         x = np.where((x >= 0) & (x < D), x, px)
         y = np.where((y >= 0) & (y < D), y, py)

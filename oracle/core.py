@@ -236,13 +236,16 @@ class StepResult:
 
 def resolve_moves(L: Layout, pos: np.ndarray, actions: Sequence[int], order: Sequence[int]) -> None:
     """core.py:274-300, in place.  `order` lists agent ids in action-dict iteration order; agents
-    not listed do not move.  Occupancy is a set of cells (a cell is freed when ANY agent leaves it,
+    not listed do not move.  An entry may be an (id, action) pair -- a dict entry with its own
+    action, as core.py:279-281 reads them (int(key) indexes like numpy, so '-1' is agent n-1 and
+    one agent named under two keys moves twice); a plain id takes actions[id].  Occupancy is a set of cells (a cell is freed when ANY agent leaves it,
     even if another agent still stands there); `forbidden` holds (from, to) cell pairs that later
     movers may not take (reverse of every accepted move, plus both crossing diagonals)."""
     occupied = {(int(x), int(y)) for x, y in pos}
     forbidden = set()
     for i in order:
-        dx, dy = move_delta(actions[i])
+        i, a = (i if isinstance(i, tuple) else (i, actions[i]))
+        dx, dy = move_delta(a)
         px, py = int(pos[i, 0]), int(pos[i, 1])
         x, y = px + dx, py + dy
         if not 0 <= x < L.D:
@@ -399,10 +402,9 @@ class OracleWarehouse:
         return obs_dicts(self.layout, observe(self.layout, self.state))
 
     def step(self, action_dict: Dict[str, int]):
-        order: List[int] = [int(k) for k in action_dict]
+        # every entry with its own key and action, as core.py:279-281 reads them
+        order = [(int(k), int(a)) for k, a in action_dict.items()]
         acts = np.zeros(self.num_agents, np.int64)
-        for k, a in action_dict.items():
-            acts[int(k)] = int(a)
         res = step(self.layout, self.state, acts, order, self.draws)
         obs = obs_dicts(self.layout, observe(self.layout, self.state))
         rewards = {str(i): res.rewards[i] for i in range(self.num_agents)}

@@ -1,17 +1,25 @@
-// wh_version(): library identification, tying a built binary to the kernel sources it came from.
-// WH_SOURCE_SHA is the first 16 hex digits of sha256 over csrc/*.hip and csrc/*.h concatenated in
-// sorted name order (the Makefile computes it; bench.py:source_sha and warehouse/_native.py compute
-// the same hash from the tree), so a stale library is detected before it is trusted.
+// wh_version(): library identification, tying a built binary to the sources and settings it came from.
+// WH_SOURCE_SHA is the first 16 hex digits of sha256 over csrc/*.hip, *.h, *.cpp and the Makefile
+// (sorted names), then include/warehouse_amd.h (the Makefile computes it; warehouse/_native.py and
+// bench.py compute the same hash from the tree).  WH_VARIANT lists the build settings that did not
+// come from the Makefile (e.g. EXTRA=-DWH_ABLATION), empty for the production build, so a stale or
+// variant library is detected before it is trusted.
 #include "warehouse_amd.h"
 
 #ifndef WH_SOURCE_SHA
 #define WH_SOURCE_SHA "unknown"
 #endif
+#ifndef WH_VARIANT
+#define WH_VARIANT ""
+#endif
+
+#ifdef WH_CHECK
+#define WH_MODE "(assert mode) "
+#else
+#define WH_MODE ""
+#endif
 
 extern "C" const char* wh_version(void) {
-#ifdef WH_CHECK
-  return "warehouse_amd gfx950 lane-per-env v3 (assert mode) sha=" WH_SOURCE_SHA;
-#else
-  return "warehouse_amd gfx950 lane-per-env v3 sha=" WH_SOURCE_SHA;
-#endif
+  return sizeof(WH_VARIANT) > 1 ? "warehouse_amd gfx950 lane-per-env v3 " WH_MODE "sha=" WH_SOURCE_SHA " variant=" WH_VARIANT
+                                : "warehouse_amd gfx950 lane-per-env v3 " WH_MODE "sha=" WH_SOURCE_SHA;
 }

@@ -274,13 +274,6 @@ struct Lds {
   // Agent words when processing in action-dict order; afterwards the reward-row staging area.
   // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
   alignas(16) uint32_t agl[C::NAM][BT];
-  // Reset slots (fused rollout): lane tid's NEXT episode's reset state, precomputed for the whole
-  // wave at once (reset_philox<..., TO_SLOT>) and consumed when the lane ends its episode
-  // (reset_from_slot): agent words, R requests (point | (target + 1) << 8), open mask, header, and
-  // the episode the slot was computed for (valid iff rs_ep == epi + 1).
-  uint32_t rs_ag[C::NAM][BT];
-  uint16_t rs_req[C::R][BT];
-  uint32_t rs_am[2][BT], rs_hdr[BT], rs_ep[BT];
   // Cell (x | y << 16) -> pickup index + 1, 0 for other cells: one v_perm (the byte index
   // x | y << 8) + one ds_read_u8; the point's row in pkp is then one v_lshl_add away (row_byte).
   __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
@@ -315,6 +308,19 @@ struct Lds {
   // is one AND of the (idle: 0xFF target bytes) agent word.
   __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const { return tbl[C::T.dst / 4 - 1 + tb]; }
 };
+
+// Reset slots (fused rollout only: their own __shared__ object in that k_step instance, so the
+// other step instances and k_reset do not carry them): lane tid's NEXT episode's reset state,
+// precomputed for the whole wave at once (reset_philox<..., TO_SLOT>) and consumed when the lane ends
+// its episode (reset_from_slot): agent words, R requests (point | (target + 1) << 8), open mask,
+// header, and the episode the slot was computed for (valid iff rs_ep == epi + 1).
+template <class C>
+struct Slots {
+  uint32_t rs_ag[C::NAM][BT];
+  uint16_t rs_req[C::R][BT];
+  uint32_t rs_am[2][BT], rs_hdr[BT], rs_ep[BT];
+};
+struct NoSlots {};
 
 // Every 16-byte load of a lane is issued before its first LDS write, so the prologue pays one
 // memory round trip.  (A strided `for` loop over words compiled to load -> vmcnt(0) -> ds_write per
@@ -439,7 +445,8 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 // instead of its registers and pickup plane, for episode epi + 1.
 template <class C, int NAC = -1, bool TO_SLOT = false>
 __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
-                                             int na_rt, int variable_n, uint32_t W, int tid) {
+                                             int na_rt, int variable_n, uint32_t W, int tid,
+                                             Slots<C>* RS = nullptr) {
   WH_PHASE_MARK(reset);
   const uint32_t ep = s.epi + 1u;
   const int na = NAC >= 0 ? NAC : na_rt;
@@ -463,7 +470,7 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
       const uint32_t cell = L.valid_cell(v);
       a = (i < (int)n) ? (cell | IDLE) : IDLE;
     }
-    if (TO_SLOT) L.rs_ag[i][tid] = a;
+    if (TO_SLOT) RS->rs_ag[i][tid] = a;
     else s.ag[i] = a;
   }
   if (!TO_SLOT) {
@@ -497,11 +504,11 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
     for (int i = j + 1; i < C::R; ++i) tg[i] += 1u - ((tg[i] - tg[j]) >> 31);   // + (tg[i] >= tg[j])
   if (TO_SLOT) {
 #pragma unroll
-    for (int j = 0; j < C::R; ++j) L.rs_req[j][tid] = (uint16_t)(sel[j] | ((tg[j] + 1u) << 8));
-    L.rs_am[0][tid] = plo;
-    L.rs_am[1][tid] = phi;
-    L.rs_hdr[tid] = (n << 16) | (1u << 24);
-    L.rs_ep[tid] = ep;
+    for (int j = 0; j < C::R; ++j) RS->rs_req[j][tid] = (uint16_t)(sel[j] | ((tg[j] + 1u) << 8));
+    RS->rs_am[0][tid] = plo;
+    RS->rs_am[1][tid] = phi;
+    RS->rs_hdr[tid] = (n << 16) | (1u << 24);
+    RS->rs_ep[tid] = ep;
   } else {
 #pragma unroll
     for (int j = 0; j < C::R; ++j) L.pkp[sel[j]][tid] = (uint16_t)((tg[j] + 1u) | wexp);
@@ -518,14 +525,14 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
 // Bit-identical to reset_philox<C, NA> (plus the occupancy clear) for that env, for ~40 issue slots
 // instead of a Philox block per lane, a Floyd chain on wave-uniform values and the rank decode.
 template <class C, int NA>
-__device__ __forceinline__ void reset_from_slot(Regs<C>& s, Lds<C>& L, uint32_t W, int tid, int l) {
+__device__ __forceinline__ void reset_from_slot(Regs<C>& s, Lds<C>& L, const Slots<C>& RS, uint32_t W, int tid, int l) {
   WH_PHASE_MARK(slot_reset);
   const int lane = tid & 63;
   const int col = (tid & ~63) + l;
   const uint32_t me = mask_z((uint32_t)(lane ^ l));
-  const uint32_t av = L.rs_ag[lane < NA ? lane : 0][col];
-  const uint32_t rq = L.rs_req[lane < C::R ? lane : 0][col];
-  const uint32_t alo = L.rs_am[0][col], ahi = L.rs_am[1][col], hdr = L.rs_hdr[col];
+  const uint32_t av = RS.rs_ag[lane < NA ? lane : 0][col];
+  const uint32_t rq = RS.rs_req[lane < C::R ? lane : 0][col];
+  const uint32_t alo = RS.rs_am[0][col], ahi = RS.rs_am[1][col], hdr = RS.rs_hdr[col];
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i)
     s.ag[i] = msel(me, i < NA ? (uint32_t)__builtin_amdgcn_readlane(av, i) : IDLE, s.ag[i]);
@@ -915,11 +922,15 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
 #pragma unroll
         for (int sidx = 0; sidx < C::NAM; ++sidx) {
-          int who = (sidx < na) ? order[e * na + sidx] : -1;
+          // entry: agent id in bits 0-7, optionally the slot's own action + 1 in bits 8-15 (a dict
+          // naming one agent under two keys moves it once per key, with that key's action)
+          const int32_t raw = (sidx < na) ? order[e * na + sidx] : -1;
+          int who = raw < 0 ? -1 : (raw & 0xFF);
+          const uint32_t sact = raw < 0 ? 0u : ((uint32_t)raw >> 8) & 0xFFu;
           const bool live = who >= 0 && who < (int)n && who < C::NAM;
           who = live ? who : 0;
           const uint32_t a = L.agl[who][tid];
-          const uint32_t mv = live ? (uint32_t)actions_g[e * na + who] : 4u;
+          const uint32_t mv = live ? (sact ? sact - 1u : (uint32_t)actions_g[e * na + who]) : 4u;
           const uint32_t p = a & XY16;
           const uint32_t c = step16<C::D>(p, L.mv(mv > 8u ? 4u : mv));
           const bool occupied = (L.occ[c >> 16][tid] >> (c & 31u)) & 1u;
@@ -1485,9 +1496,11 @@ __device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]
   }
 }
 
-template <class C, int POLICY>
-__device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, Lds<C>& L, const Keys& k,
-                                               uint32_t gid, int64_t e, int tid) {
+// SLOTS = false (the fused sampler step, k_sampler: one step per launch): no reset slots -- a lone
+// ending lane is reset by reset_lane, as the 1-step launches of k_step do (kSlotMinSteps).
+template <class C, int POLICY, bool SLOTS = true>
+__device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, Lds<C>& L, Slots<C>* RS,
+                                               const Keys& k, uint32_t gid, int64_t e, int tid) {
 #ifdef WH_ABLATION
   const int ablate = a.ablate;
 #else
@@ -1520,14 +1533,16 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
       // at a time (every lane takes part, so not in a tail wave whose lanes past B have exited)
       const bool full = __ballot(true) == ~0ull;
 #ifndef WH_NO_RESET_SLOTS   // (A/B builds: -DWH_NO_RESET_SLOTS resets one lane from scratch)
-      if (a.steps >= kSlotMinSteps && __popcll(dm) <= kSlotResetMax && full) {
+      if (SLOTS && a.steps >= kSlotMinSteps && __popcll(dm) <= kSlotResetMax && full) {
         // their precomputed next-episode states, after (re)filling the wave's slots if one of
         // theirs is stale: one wave-wide fill (every lane's next episode) serves the resets of
         // the lanes that end later in this launch
-        if (__any(done && L.rs_ep[tid] != s.epi + 1u))
-          reset_philox<C, C::NAM, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
-        for (uint64_t m = dm; m; m &= m - 1ull) reset_from_slot<C, C::NAM>(s, L, (uint32_t)a.W, tid, __builtin_ctzll(m));
-        lg.rebuild = lg.rebuild || done;   // their grid columns were cleared
+        if constexpr (SLOTS) {
+          if (__any(done && RS->rs_ep[tid] != s.epi + 1u))
+            reset_philox<C, C::NAM, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid, RS);
+          for (uint64_t m = dm; m; m &= m - 1ull) reset_from_slot<C, C::NAM>(s, L, *RS, (uint32_t)a.W, tid, __builtin_ctzll(m));
+          lg.rebuild = lg.rebuild || done;   // their grid columns were cleared
+        }
       } else
 #endif
       if (__popcll(dm) == 1 && full) {
@@ -1564,6 +1579,7 @@ __device__ unsigned long long g_wh_times[kTimeWaves * kTimeSlots];
 template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
+  __shared__ std::conditional_t<FAST, Slots<C>, NoSlots> RS;   // reset slots: fused rollout only
   const int tid = threadIdx.x;
   if (FAST) WH_T(0);
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
@@ -1589,7 +1605,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
 #pragma unroll
   for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
-  if (FAST) L.rs_ep[tid] = s.epi;                       // reset slots start stale (!= epi + 1)
+  if constexpr (FAST) RS.rs_ep[tid] = s.epi;            // reset slots start stale (!= epi + 1)
   if (FAST) WH_T(2);
 
   if (!FAST && a.phase == PH_POLICY) {
@@ -1602,8 +1618,8 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     return;
   }
 
-  if (FAST)
-    run_steps_fast<C, POLICY>(a, s, L, k, gid, e, tid);
+  if constexpr (FAST)
+    run_steps_fast<C, POLICY>(a, s, L, &RS, k, gid, e, tid);
   else if (!ORDERED && a.phase == PH_ALL)
     run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
   else
@@ -1667,13 +1683,13 @@ struct ObsSrc {
   static constexpr int L = 9 * R + 1, W = (NAM * L + 3) / 4;
   uint32_t w[2][W];
 };
-template <int R, int NAM>
+template <int R, int NAM, int A0 = 1, int G0 = 1 + R, int P0 = 1 + 3 * R, int Q0 = 1 + 5 * R>
 constexpr ObsSrc<R, NAM> make_obs_src() {
   ObsSrc<R, NAM> t{};
   constexpr int L = 9 * R + 1;
   for (int fr = 0; fr < 2; ++fr)
     for (int k = 0; k < NAM * L; ++k)
-      t.w[fr][k >> 2] |= obs_src<R>(k / L, k % L, fr != 0) << (8 * (k & 3));
+      t.w[fr][k >> 2] |= obs_src<R, A0, G0, P0, Q0>(k / L, k % L, fr != 0) << (8 * (k & 3));
   return t;
 }
 template <int R, int NAM>
@@ -1836,6 +1852,137 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(O.src[lim >> 31]);
       out[o] = k < (lim & 0x7FFFFFFFu) ? (float)O.img[el1][sb[k]] : 0.0f;
     }
+  }
+}
+
+// ----------------------------------------------------------------------------- fused sampler step
+// The sampler route (wh_sampler_step: device policy + step + auto-reset, then the observation rows)
+// as ONE launch.  A workgroup of 2 x BT lanes owns BT envs: lanes [0, BT) run the fused rollout's
+// step for one env each (exactly k_step's fast instance, one step, lane = env), and write their
+// env's byte image straight from the registers and the pickup plane; then all 2 x BT lanes stream the
+// group's contiguous rows [BT x NA x L] f32 from the images, as k_observe's write loop does.
+// Against k_step + k_observe: no second launch, no re-read of the state, no per-env image pass.
+// Measured write phase of this shape (tools/obs_write_probe.hip, Medium-8): 512 lanes and 256 envs
+// per workgroup stream at the constant-store ceiling (6.45 TB/s); 256 lanes alone (the step
+// launch's own shape) reach half of it, so the second half of the workgroup is what makes the rows
+// fast.  Two waves per SIMD cap the step code at 256 registers per lane.
+//
+// Image layout (FImg): word/half-word aligned sections so the step lanes write them with b16/b32
+// stores; the compile-time gather table kObsSrcF uses the same offsets.
+template <int R>
+struct FImg {
+  static constexpr int A0 = 1, G0 = (R + 2) & ~1, P0 = G0 + 2 * R, Q0 = (P0 + 2 * R + 3) & ~3,
+                       IMG = Q0 + 4 * R;
+  static_assert(IMG <= 256, "image byte offsets are 8-bit gather indices");
+};
+template <int R, int NAM>
+__constant__ ObsSrc<R, NAM> kObsSrcF =
+    make_obs_src<R, NAM, FImg<R>::A0, FImg<R>::G0, FImg<R>::P0, FImg<R>::Q0>();
+
+template <class C>
+struct SampLds {
+  static constexpr int IMG = FImg<C::R>::IMG, SRCW = ObsSrc<C::R, C::NAM>::W;
+  alignas(16) uint8_t img[BT][IMG];
+  uint32_t lim[BT];        // n * L (floats of live rows) | fresh << 31
+  uint32_t src[2][SRCW];
+};
+
+// core.py:224-260 / 371-432 for the env of this lane, from its registers after the step: the image
+// k_observe builds from the packed state (n, availability, delivery targets, positions, the open
+// requests in ascending pickup order with their pickup and delivery cells).
+template <class C>
+__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid) {
+  using F = FImg<C::R>;
+  uint8_t* im = O.img[tid];
+  const uint32_t n = (s.hdr >> 16) & 0xFFu;
+  const bool fresh = (s.hdr >> 24) & 1u;
+  constexpr uint32_t nul = (uint32_t)(C::D / 2), nul2 = nul | (nul << 8);
+  im[0] = (uint8_t)n;
+#pragma unroll
+  for (int r = 0; r < C::R; ++r) {
+    const uint32_t a = r < C::NAM ? s.ag[r] : IDLE;
+    const bool live = (uint32_t)r < n;
+    const bool carry = (a & 0xFF00u) != 0xFF00u;
+    im[F::A0 + r] = (uint8_t)((live && !fresh && !carry) ? 1 : 0);
+    const uint32_t dtg = __builtin_amdgcn_perm(a, a, 0x0C0C0301u);   // dx | dy << 8
+    const uint32_t pos = __builtin_amdgcn_perm(a, a, 0x0C0C0200u);   // x | y << 8
+    *reinterpret_cast<uint16_t*>(im + F::G0 + 2 * r) = (uint16_t)((live && !fresh && carry) ? dtg : nul2);
+    *reinterpret_cast<uint16_t*>(im + F::P0 + 2 * r) = (uint16_t)(live ? pos : nul2);
+  }
+  // open requests, ascending pickup index (core.py:409-418); fewer than R open (never after a
+  // reset or a step) leaves zero slots, as k_observe does
+  uint32_t mlo = (uint32_t)s.am, mhi = (uint32_t)(s.am >> 32);
+#pragma unroll
+  for (int r = 0; r < C::R; ++r) {
+    uint32_t flo, fhi;
+    asm("v_ffbl_b32 %0, %1" : "=v"(flo) : "v"(mlo));   // 0xFFFFFFFF when empty
+    asm("v_ffbl_b32 %0, %1" : "=v"(fhi) : "v"(mhi));
+    const uint32_t j = __builtin_elementwise_min(
+        __builtin_elementwise_min(flo, __builtin_elementwise_add_sat(fhi, 32u)), (uint32_t)C::P);
+    const uint32_t rp = L.rtag(j).x;                        // pickup cell x | y << 16
+    const uint32_t tb = L.target_byte(j, tid);              // target + 1 (row P: scratch)
+    const uint32_t dc = L.dst_tb(tb);                       // x << 8 | y << 24 | 0x00FF00FF
+    const uint32_t w = __builtin_amdgcn_perm(dc, rp, 0x07050200u);   // px | py << 8 | dx << 16 | dy << 24
+    *reinterpret_cast<uint32_t*>(im + F::Q0 + 4 * r) = j < (uint32_t)C::P ? w : 0u;
+    uint64_t m = ((uint64_t)mhi << 32) | mlo;
+    m &= m - 1ull;
+    mlo = (uint32_t)m;
+    mhi = (uint32_t)(m >> 32);
+  }
+  O.lim[tid] = n * (uint32_t)C::L | (fresh ? 0x80000000u : 0u);
+}
+
+template <class C, int POLICY>
+__global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restrict__ obs) {
+  __shared__ Lds<C> L;
+  __shared__ SampLds<C> O;
+  const int tid = threadIdx.x;
+  const bool stepper = tid < BT;
+  const int64_t e0 = (int64_t)blockIdx.x * BT;
+  const int64_t e = e0 + tid;
+  const bool live = stepper && e < a.B;
+  RawEnv<C> raw;
+  if (live) load_env_issue<C>(raw, a.state, a.B, e, C::NAM);
+  if (stepper) {
+    load_tables<C>(L.tbl, a.tables);
+  } else {
+    const uint32_t* srcg = &kObsSrcF<C::R, C::NAM>.w[0][0];
+    for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
+  }
+  __syncthreads();
+  if (live) {
+    const Keys k{a.k0, a.k1};
+    const uint32_t gid = (uint32_t)(a.env_offset + e);
+    Regs<C> s;
+    load_env_finish<C>(s, L, raw, (uint32_t)a.W, tid);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): drain the state loads before the step (k_step)
+#pragma unroll
+    for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+    run_steps_fast<C, POLICY, false>(a, s, L, nullptr, k, gid, e, tid);
+    store_env<C>(s, L, a.state, a.B, e, C::NAM, tid);
+    write_image<C>(s, L, O, tid);
+  }
+  __syncthreads();
+  // rows of the group's envs: one contiguous [nenv x NA x L] f32 region, float4 per lane (NA * L
+  // % 4 == 0 and obs 16-byte aligned: checked on the host)
+  const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
+  constexpr uint32_t qe = (uint32_t)(C::NAM * C::L / 4);
+  constexpr uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
+  const uint32_t total = nenv * qe;
+  f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * (int64_t)(C::NAM * C::L));
+  for (uint32_t q = tid; q < total; q += 2 * BT) {
+    const uint32_t el4 = __umulhi(q, magic);
+    const uint32_t k4 = q - el4 * qe;
+    const uint32_t lim = O.lim[el4];
+    const uint32_t sw = O.src[lim >> 31][k4];
+    const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
+    const uint8_t* im = O.img[el4];
+    f32x4 v;
+    v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
+    v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
+    v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
+    v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
+    out4[q] = v;
   }
 }
 
@@ -2060,6 +2207,7 @@ struct Kernels {
   void (*step[3])(StepParams);
   void (*step_fast[3])(StepParams);   // [policy]: greedy / random fused rollouts (NAM even), else null
   void (*step_ordered)(StepParams);
+  void (*sampler[3])(StepParams, float*);   // [policy]: fused step + rows (k_sampler), NAM even, else null
   void (*reset)(ResetParams);
   void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // 8 / 16 / 64 envs per WG
   int tblw, nv;
@@ -2074,11 +2222,15 @@ Kernels make_kernels() {
   k.step[1] = k_step<C, POL_GREEDY, false, false>;
   k.step[2] = k_step<C, POL_RANDOM, false, false>;
   k.step_fast[0] = nullptr;
+  k.sampler[0] = nullptr;
   if constexpr (NAM % 2 == 0) {
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
+    k.sampler[1] = k_sampler<C, POL_GREEDY>;
+    k.sampler[2] = k_sampler<C, POL_RANDOM>;
   } else {
     k.step_fast[1] = k.step_fast[2] = nullptr;
+    k.sampler[1] = k.sampler[2] = nullptr;
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
@@ -2493,11 +2645,22 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
   a.phase = PH_ALL;
   a.autoreset = 1;
   a.variable_n = variable_n ? 1 : 0;
-  // the step launch (the fused rollout instance when its outputs allow) and the observation
-  // kernel: a step launch holds one workgroup per CU, too few waves to stream 2.6 KB of rows per
-  // env near the write ceiling (measured: 2.7 TB/s as an epilogue of the step launch against
-  // k_observe's 5.7 TB/s), so the rows stay with k_observe's small workgroups
-  int rc = launch_step(cfg, B, state, policy, a, stream);
+  wh_launch l;
+  int rc = resolve_step(cfg, B, state, policy, a, stream, &l);
+  if (rc) return rc;
+  // One launch (k_sampler: the fused rollout's step on half of each workgroup, then the rows by
+  // all of it) when the fast step instance applies and the rows are whole float4s; otherwise the
+  // step launch and k_observe.  WH_SAMPLER_UNFUSED=1 forces the two launches (A/B runs).
+  static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
+  Geometry g;
+  const Kernels* k = nullptr;
+  const uint32_t* tab = nullptr;
+  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && l.kern == k->step_fast[policy] &&
+      k->sampler[policy] && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+    hipLaunchKernelGGL(k->sampler[policy], grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
+    return hip_err(hipGetLastError());
+  }
+  rc = enqueue(l);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
 }

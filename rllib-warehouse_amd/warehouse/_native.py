@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
 from typing import Optional
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
@@ -108,8 +109,15 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C rllib-warehouse_amd/csrc` (there is no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
+    # Every entry point of include/warehouse_amd.h must be there: argtypes applied to an older build
+    # whose signatures differ would turn a missing argument into out-of-bounds device writes.  Only
+    # explicit A/B experiments (WAREHOUSE_AMD_AB=1, tools/ab.sh) may load a library lacking some.
+    missing = [s for s in SYMBOLS if not hasattr(L, s)]
+    if missing and os.environ.get("WAREHOUSE_AMD_AB") != "1":
+        raise WarehouseNativeError(f"{LIB_PATH} lacks entry points {missing}: built from other sources "
+                                   "-- rebuild (__graft_entry__.build())")
 
-    class _Sigs:   # argtypes for the exported symbols (an A/B build of another version may lack some)
+    class _Sigs:   # (A/B builds only) argtypes of a symbol the library lacks go nowhere
         def __setattr__(self, name, val):
             pass
 
@@ -155,49 +163,84 @@ def lib() -> ctypes.CDLL:
 
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(CSRC)), "include", "warehouse_amd.h")
+# the one variant an extra library may carry (build_ab/check.so: the assert-mode kernels)
+CHECK_VARIANT = "EXTRA=-DWH_CHECK"
 
 
-def tree_source_sha(csrc: str = CSRC) -> str:
-    """sha256 (16 hex digits) of csrc/*.hip + csrc/*.h in sorted name order: the hash the Makefile
-    bakes into wh_version() and bench.py:source_sha() ties the committed profiles to."""
+def hashed_files(csrc: str = CSRC, header: str = HEADER):
+    """The files the library's code depends on, in the order the Makefile hashes them (HASHED):
+    csrc/*.hip, *.h, *.cpp and the Makefile in sorted name order, then include/warehouse_amd.h."""
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")) or f == "Makefile")
+    return [os.path.join(csrc, f) for f in names] + [header]
+
+
+def tree_source_sha(csrc: str = CSRC, header: str = HEADER) -> str:
+    """sha256 (16 hex digits) of hashed_files(): the hash the Makefile bakes into wh_version() and
+    bench.py:source_sha() ties the committed profiles to."""
     import hashlib
 
     h = hashlib.sha256()
-    for f in sorted(os.listdir(csrc)):
-        if f.endswith((".hip", ".h")):
-            with open(os.path.join(csrc, f), "rb") as fh:
-                h.update(fh.read())
+    for p in hashed_files(csrc, header):
+        with open(p, "rb") as fh:
+            h.update(fh.read())
     return h.hexdigest()[:16]
 
 
+_VERSION_RE = re.compile(r"lane-per-env v3 (?:\(assert mode\) )?sha=([0-9a-f]{16}|unknown)(?: variant=([^\x00]*))?")
+
+
+def parse_version(version) -> tuple:
+    """(sha, variant) of a wh_version() string ("... sha=<16 hex>[ variant=<settings>]"); variant is
+    "" for a build with the Makefile's own settings, (None, None) if the string carries no sha."""
+    v = version.decode(errors="replace") if isinstance(version, bytes) else version
+    m = _VERSION_RE.search(v)
+    return (m.group(1), (m.group(2) or "").strip()) if m else (None, None)
+
+
 def version_sha(version: bytes) -> Optional[str]:
-    """The source sha a wh_version() string carries ("... sha=<16 hex>"), or None."""
-    v = version.decode(errors="replace")
-    return v.rsplit("sha=", 1)[1].strip() if "sha=" in v else None
+    """The source sha a wh_version() string carries, or None."""
+    return parse_version(version)[0]
+
+
+def file_version(path: str) -> tuple:
+    """(sha, variant) baked into a built library file, read from its bytes (no load)."""
+    with open(path, "rb") as fh:
+        m = re.search(rb"lane-per-env v3 (?:\(assert mode\) )?sha=(?:[0-9a-f]{16}|unknown)(?: variant=[^\x00]*)?",
+                      fh.read())
+    return parse_version(m.group(0)) if m else (None, None)
 
 
 def file_source_sha(path: str) -> Optional[str]:
     """The source sha baked into a built library file, read from its bytes (no load)."""
-    import re
+    return file_version(path)[0]
 
-    with open(path, "rb") as fh:
-        m = re.search(rb"lane-per-env v3 (?:\(assert mode\) )?sha=([0-9a-f]{16}|unknown)", fh.read())
-    return m.group(1).decode() if m else None
+
+def check_provenance(version, want: str, allowed_variants=("",), what: str = "library") -> None:
+    """Raise WarehouseNativeError unless wh_version() text `version` carries sha `want` and one of
+    `allowed_variants` (the production library: none)."""
+    sha, variant = parse_version(version)
+    if sha != want:
+        raise WarehouseNativeError(f"{what} was built from sources sha={sha}, the tree has sha={want}: "
+                                   "stale library -- rebuild (__graft_entry__.build())")
+    if variant not in allowed_variants:
+        raise WarehouseNativeError(f"{what} is a variant build ({variant!r}), not the Makefile's own "
+                                   "settings -- rebuild (__graft_entry__.build())")
 
 
 def verify_provenance(extra_libs=()) -> str:
-    """Raise WarehouseNativeError unless the loaded library -- and every file in `extra_libs` (e.g.
-    the assert-mode build_ab/check.so) -- was built from the kernel sources in this tree.  Returns
-    the sha."""
+    """Raise WarehouseNativeError unless the loaded library was built from the sources in this tree
+    with the Makefile's own settings (no variant), and every file in `extra_libs` (e.g. the
+    assert-mode build_ab/check.so) from the same sources with no variant or the assert-mode one.
+    Returns the sha."""
     want = tree_source_sha()
-    got = version_sha(lib().wh_version())
-    if got != want:
-        raise WarehouseNativeError(f"{LIB_PATH} was built from sources sha={got}, the tree has sha={want}: "
-                                   "stale library -- rebuild (__graft_entry__.build())")
+    check_provenance(lib().wh_version(), want, ("",), LIB_PATH)
     for p in extra_libs:
-        g = file_source_sha(p) if os.path.exists(p) else "missing"
-        if g != want:
-            raise WarehouseNativeError(f"{p}: built from sources sha={g}, the tree has sha={want}: stale library")
+        if not os.path.exists(p):
+            raise WarehouseNativeError(f"{p}: missing")
+        sha, variant = file_version(p)
+        check_provenance(f"lane-per-env v3 sha={sha}" + (f" variant={variant}" if variant else ""), want,
+                         ("", CHECK_VARIANT), p)
     return want
 
 

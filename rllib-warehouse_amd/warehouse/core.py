@@ -40,6 +40,15 @@ def _default_device():
     return os.environ.get("WAREHOUSE_DEVICE", "cuda")
 
 
+def agent_index(key, n: int) -> int:
+    """The agent a dict key names, as core.py:280-281 indexes with it: int(key), negative values
+    wrapping like numpy (-n..-1 -> 0..n-1); IndexError outside [-n, n)."""
+    idx = int(key)
+    if not -n <= idx < n:
+        raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
+    return idx + n if idx < 0 else idx
+
+
 class Warehouse(MultiAgentEnv):
     metadata = {"render.modes": ["human", "ansi", "rgb_array"]}
 
@@ -168,14 +177,14 @@ class Warehouse(MultiAgentEnv):
         io = h_io.numpy()                                    # row 0: actions, row 1: dict order
         io[0] = 4
         io[1] = -1
+        if len(action_dict) > self._engine.agent_slots:
+            raise ValueError(f"{len(action_dict)} dict entries for {self._engine.agent_slots} agent slots")
         for s, (key, action) in enumerate(action_dict.items()):
-            idx = int(key)
+            idx = agent_index(key, n)
             a = int(action)
             if not -9 <= a <= 8:                            # MOVES[action] (core.py:282)
                 raise IndexError("list index out of range")
-            if not 0 <= idx < n:
-                raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
-            io[1, s] = idx
+            io[1, s] = idx | ((a % 9 + 1) << 8)             # the entry's own action (a repeated agent)
             io[0, idx] = a % 9                               # Python's negative-index wrap
         eng = self._engine
         if self._rendering:

@@ -28,6 +28,7 @@ import torch
 from ._compat import spaces
 from ._geometry import GEOMETRY
 from .batched import BatchedWarehouse
+from .core import agent_index
 
 # sorted gym.spaces.Dict key order and each key's flattened width, R = num_requests
 OBS_KEYS = ("num_agents", "other_availabilities", "other_delivery_targets", "other_positions",
@@ -189,7 +190,9 @@ class WarehouseBaseEnv:
         order, and an agent missing from the dict is skipped -- it neither moves nor re-marks its
         cell (a "stay" would), so a later agent may enter a cell a co-located agent just left.
         Actions wrap like Python indexing; >= 9 raises IndexError (MOVES[action], core.py:281),
-        and so does an agent id outside the env's episode (agent_positions[idx], core.py:280)."""
+        and so does an agent id outside [-n, n) (agent_positions[idx], core.py:280); negative keys
+        name agent n + key as numpy indexing does, and an agent named under two keys ('0' and 0)
+        moves once per entry with that entry's action (each order entry carries its own action)."""
         NA = self.vec.num_agents
         acts = np.full((self.num_envs, NA), 4, np.int32)
         order = np.full((self.num_envs, NA), -1, np.int32)
@@ -201,13 +204,11 @@ class WarehouseBaseEnv:
             if len(ad) > NA:
                 raise ValueError(f"env {e}: {len(ad)} actions for {NA} agent slots")
             for s, (a, v) in enumerate(ad.items()):
-                idx, v = int(a), int(v)
+                idx, v = agent_index(a, n), int(v)
                 if not -9 <= v < 9:
                     raise IndexError("list index out of range")   # MOVES[a], core.py:281
-                if not 0 <= idx < n:
-                    raise IndexError("index %d is out of bounds for axis 0 with size %d" % (idx, n))
                 acts[e, idx] = v % 9
-                order[e, s] = idx
+                order[e, s] = idx | ((v % 9 + 1) << 8)
                 ascending = ascending and idx == s
             ascending = ascending and len(ad) == n
         # the ascending kernel when every dict is full and in id order (the common sampler case),

@@ -11,7 +11,10 @@ It never runs on the GPU box and nothing imports it at test time; the tests read
   separate RandomState (so the env's global MT19937 stream is untouched), recording every draw
   the env makes (`warehouse/core.py:195-220` at reset, `:339-350` per step), the canonical state
   after reset and after every step, per-agent observations flattened in sorted-key order, rewards
-  and dones.  `ord_*` files do the same with shuffled/partial action dicts (`core.py:279`).
+  and dones.  `ord_*` files do the same with shuffled/partial action dicts (`core.py:279`);
+  `keys_*` with the key forms `int(key)` accepts beyond "0".."n-1" (`core.py:280`): int keys,
+  negative keys (numpy wraps them to n + key) and one agent named under two keys in one dict
+  (moved once per entry, each with its own action).
 * G2 `g2_<variant>.npz` -- single transitions from adversarial hand-built states (agents packed
   on a few cells, on pickup cells, carrying next to their delivery cell, timers about to expire,
   t about to reach T) with random actions and dict orders.
@@ -193,6 +196,69 @@ def run_g1(variant, n, seed, steps=200, shuffle=False):
     return arr
 
 
+def run_keys(variant, n, seed, steps=200):
+    """A G1 episode whose action dicts mix key forms: str(a), int a, str(a - n), int(a - n), so some
+    dicts name an agent under two keys (both entries act).  Per step the dict's entries are recorded
+    as key_form (0 str, 1 int, 2 negative str, 3 negative int; -1 = no entry), key_agent (the agent
+    the key names) and key_act (the entry's action, -9..8)."""
+    cls = VARIANTS[variant]
+    np.random.seed(seed)
+    act_rng = np.random.RandomState(20_000 + 31 * seed + n)
+    env = cls(n)
+    R = env._num_requests
+    with DrawRecorder() as rec:
+        obs0 = env.reset()
+        pairs, rsel, rtgt0 = reset_draws(rec.take(), R)
+    spawn = np.array(spawn_valid(env, pairs), dtype=np.int32)
+    assert np.array_equal(spawn, env._agent_positions)
+    out = {k: [] for k in ("key_form", "key_agent", "key_act", "n_inactive", "k", "rpos", "rtgt", "rsel",
+                           "pos", "agent_tgt", "pk_tgt", "pk_timer", "t", "obs", "rewards", "done")}
+    s0 = canon_state(env)
+    dup_steps = 0
+    for s in range(steps):
+        m = int(act_rng.randint(1, n + 1))
+        form = np.full(n, -1, np.int32)
+        agent = np.full(n, -1, np.int32)
+        act = np.zeros(n, np.int32)
+        action_dict = {}
+        for j in range(m):
+            a, f, v = int(act_rng.randint(0, n)), int(act_rng.randint(0, 4)), int(act_rng.randint(-9, 9))
+            key = [str(a), a, str(a - n), a - n][f]
+            if key in action_dict:
+                continue
+            form[len(action_dict)], agent[len(action_dict)], act[len(action_dict)] = f, a, v
+            action_dict[key] = v
+        dup_steps += len({int(k) % n for k in action_dict}) < len(action_dict)
+        with DrawRecorder() as rec:
+            obs, rew, dones, infos = env.step(action_dict)
+            nin, k, rpos, rtgt, ssel = step_draws(rec.take(), R)
+        st = canon_state(env)
+        out["key_form"].append(form)
+        out["key_agent"].append(agent)
+        out["key_act"].append(act)
+        out["n_inactive"].append(nin)
+        out["k"].append(k)
+        out["rpos"].append(rpos)
+        out["rtgt"].append(rtgt)
+        sel = np.full(R, -1, np.int32)
+        sel[:k] = ssel
+        out["rsel"].append(sel)
+        for key in ("pos", "agent_tgt", "pk_tgt", "pk_timer", "t"):
+            out[key].append(st[key])
+        out["obs"].append(flat_obs(obs, n))
+        out["rewards"].append(np.array([rew[str(i)] for i in range(n)], np.float32))
+        out["done"].append(bool(dones["__all__"]))
+    assert dup_steps > 10, dup_steps
+    arr = {k: np.stack([np.asarray(v) for v in vals]) for k, vals in out.items()}
+    arr.update(
+        variant=np.array(variant), n=np.int32(n), seed=np.int32(seed),
+        spawn_pairs=np.array(pairs, np.int32), spawn=spawn, reset_sel=rsel, reset_tgt=rtgt0,
+        reset_obs=flat_obs(obs0, n),
+        **{"reset_" + k: v for k, v in s0.items()},
+    )
+    return arr
+
+
 def dense_state(env, rng):
     """An adversarial pre-step state: agents crowded on a few cells near pickups/deliveries."""
     D, n = env._area_dimension, env._num_agents
@@ -327,6 +393,13 @@ def run_g3():
     return out
 
 
+def main_keys():
+    for variant, n in (("small", 4), ("medium", 8), ("large", 16)):
+        arr = run_keys(variant, n, 7)
+        np.savez_compressed(os.path.join(HERE, f"keys_{variant}_n{n}_s7.npz"), **arr)
+    print("wrote keys_* fixtures to", HERE)
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     for variant, nmax in (("small", 4), ("medium", 9), ("large", 16)):
@@ -343,4 +416,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["keys"]:   # (added in round 4: only the keys_* fixtures)
+        main_keys()
+    else:
+        main()
+        main_keys()

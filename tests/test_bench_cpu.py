@@ -33,3 +33,23 @@ def test_profiles_are_pinned_to_the_kernel_sources(tmp_path, monkeypatch):
     assert len(sha) == 16
     # an entry from other sources is not reported
     assert bench.load_profile("no_such_tag") is None
+
+
+def test_step_roofline_names_the_binding_resource(monkeypatch):
+    """roofline.valu = SQ_INSTS_VALU per launch / kernel time against 1,024 SIMDs x 1.2 G wave64-VALU/s;
+    `bound` is the larger of the VALU and HBM fractions, both reported."""
+    prof = {"avg_ns": 50_000.0, "bytes_per_launch": 5.8e7, "steps_per_launch": 20,
+            "sq": {"SQ_INSTS_VALU": 1.8e7, "SQ_WAVES": 1024.0, "SQ_WAVE_CYCLES": 2.8e7, "SQ_INSTS_LDS": 1.5e6,
+                   "SQ_WAIT_ANY": 7e6}}
+    monkeypatch.setattr(bench, "load_profile", lambda tag: prof)
+    m = dict(achieved_gbs=1000.0, kernel_ms=0.05, launches=1, steps_per_launch=20, bytes_per_launch=5.8e7,
+             bytes_per_env_step=44.0, host_fixed_us=14.0)
+    r = bench.step_roofline(m, "medium", 8, "greedy", "fused")
+    want = 1.8e7 / 50e-6 / 1e9 / (1024 * 1.2)
+    assert r["valu"]["frac"] == r["valu_frac"] and abs(r["valu_frac"] - want) < 1e-12
+    assert r["frac"] == r["hbm_frac"] == 1000.0 / 8000.0 and r["unit"] == "GB/s"
+    assert r["bound"] == "valu" and r["valu_frac"] > r["hbm_frac"]
+    assert abs(r["issue"]["single_wave_issue_occupancy"] - 1.8e7 / 2.8e7) < 1e-12
+    monkeypatch.setattr(bench, "load_profile", lambda tag: None)
+    r = bench.step_roofline(m, "medium", 8, "greedy", "fused")
+    assert r["bound"] == "hbm" and r["valu"] is None

@@ -63,6 +63,13 @@ def _worker(rank, world, port, B, steps, out):
     if r == 0:
         np.save(out, np.concatenate([g.numpy() for g in gathered]))
         np.save(out + ".meta.npy", np.array([elapsed, tot.item(), rate]))
+        # rank 0's line at world size 2 carries the host-core baseline of the same run (bench.report)
+        import argparse
+        import json
+
+        args = argparse.Namespace(no_cpu_baseline=False, cpu_procs=1, cpu_seconds=0.3, variant="medium", agents=8)
+        line = bench.report({"metric": bench.METRIC, "value": rate, "n_gpus": w}, args)
+        json.dump(line, open(out + ".line.json", "w"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,6 +83,13 @@ def test_two_rank_shards_equal_single_batch(tmp_path):
     elapsed, total, rate = np.load(out + ".meta.npy")
     assert elapsed >= 0.4                              # max over ranks: rank 1 slept 0.4 s
     assert rate == pytest.approx(world * B * 8 * steps / elapsed)
+    import json
+
+    line = json.load(open(out + ".line.json"))
+    assert line["n_gpus"] == 2
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port" and "oracle/core.py" in cb["sample"]
+    assert line["gpu_over_cpu"] == pytest.approx(rate / cb["value"])
     L = oc.layout_for("medium")
     S = ob.BState.zeros(L, world * B, 8)
     d = ob.PhiloxDraws(1234, np.arange(world * B))

@@ -338,6 +338,34 @@ def test_dropin_dict_order_negative_actions(wh):
         env.step({"0": 9})
 
 
+@pytest.mark.parametrize("variant,n", [("small", 4), ("medium", 8), ("large", 16)])
+def test_dropin_key_forms_match_reference(wh, variant, n):
+    """keys_* fixtures (the reference run with int keys, negative keys and one agent named under
+    two keys in a dict, core.py:279-281): the drop-in class, global numpy stream, equals the
+    reference's observations, rewards and dones at every step."""
+    from keyforms import key_dict
+
+    g = np.load(os.path.join(GOLDEN, f"keys_{variant}_n{n}_s7.npz"))
+    np.random.seed(int(g["seed"]))
+    env = {"small": wh.WarehouseSmall, "medium": wh.WarehouseMedium, "large": wh.WarehouseLarge}[variant](n)
+    env.reset()
+    dup = 0
+    for s in range(len(g["t"])):
+        d = key_dict(g["key_form"][s], g["key_agent"][s], g["key_act"][s], n)
+        dup += len({int(k) % n for k in d}) < len(d)
+        obs, rew, dones, _ = env.step(d)
+        flat = np.stack([np.concatenate([np.asarray(obs[str(i)][k]).ravel() for k in oc.OBS_KEYS])
+                         for i in range(n)])
+        np.testing.assert_array_equal(flat, g["obs"][s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(np.array([rew[str(i)] for i in range(n)]), g["rewards"][s])
+        assert dones["__all__"] == bool(g["done"][s])
+    assert dup > 10
+    with pytest.raises(IndexError):
+        env.step({str(-n - 1): 0})
+    with pytest.raises(IndexError):
+        env.step({str(n): 0})
+
+
 def test_dropin_train_variant_matches_oracle(wh):
     """Train variants re-draw N from the global stream at construction and every reset."""
     def run(make):

@@ -1,5 +1,7 @@
 """GPU parity of the sampler path (wh_vector_step, episode metrics) and the RLlib-facing adapters
 (warehouse.vector) against the oracle with the philox draw contract.  Bit-exact throughout."""
+import os
+
 import numpy as np
 import pytest
 
@@ -328,6 +330,46 @@ def test_base_env_replays_reference_dict_order_fixtures(wh, variant):
         np.testing.assert_array_equal(be.vec.env.observe().cpu().numpy(), ob.observe(L, S))
 
 
+@pytest.mark.parametrize("variant,n", [("small", 4), ("medium", 8), ("large", 16)])
+def test_base_env_key_forms_match_reference(wh, variant, n):
+    """keys_* fixtures (int, negative and repeated keys in one dict, core.py:279-281) replayed through
+    WarehouseBaseEnv.send_actions as one batch (env s holds the reference's state before step s):
+    positions, carried targets, rewards and dones equal the reference's; the whole transition with
+    the philox regeneration and the rows equals the batched oracle's on the encoded order entries."""
+    from keyforms import encoded_order, key_dict
+
+    from warehouse.vector import WarehouseBaseEnv
+
+    L = oc.layout_for(variant)
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"keys_{variant}_n{n}_s7.npz"))
+    steps = len(g["t"])
+    pre = fixture_pre_states(g)
+    be = WarehouseBaseEnv(variant, steps, n, train=False, seed=9)
+    be.vec.env.from_canonical(pre)
+    be._n[:] = n
+    dicts = {s: key_dict(g["key_form"][s], g["key_agent"][s], g["key_act"][s], n) for s in range(steps)}
+    be.send_actions(dicts)
+    _, rew, dones, _, _ = be.poll()
+    c = {k: v.cpu().numpy() for k, v in be.vec.env.to_canonical().items()}
+    for s in range(steps):
+        msg = f"step {s}"
+        np.testing.assert_array_equal(c["pos"][s], g["pos"][s], err_msg=msg)
+        np.testing.assert_array_equal(c["agent_target"][s], g["agent_tgt"][s], err_msg=msg)
+        assert [rew[s][str(i)] for i in range(n)] == list(g["rewards"][s]), msg
+        assert dones[s]["__all__"] == bool(g["done"][s]), msg
+    S = ob.BState(pos=pre["pos"].copy(), agent_tgt=pre["agent_target"].copy(),
+                  pk_tgt=pre["pickup_target"].copy(), pk_timer=pre["pickup_timer"].copy(),
+                  t=pre["t"].astype(np.int64), n=pre["n"].copy(), fresh=np.zeros(steps, bool),
+                  episode=np.zeros(steps, np.uint32))
+    order = np.array([encoded_order(dicts[s], n, n) for s in range(steps)], np.int32)
+    orew, _, _, _ = ob.step(L, S, np.full((steps, n), 4, np.int32), ob.PhiloxDraws(9, np.arange(steps)), order=order)
+    np.testing.assert_array_equal(np.array([[rew[s][str(i)] for i in range(n)] for s in range(steps)]), orew)
+    for f, k in (("pos", "pos"), ("agent_target", "agent_tgt"), ("pickup_target", "pk_tgt"),
+                 ("pickup_timer", "pk_timer"), ("t", "t")):
+        np.testing.assert_array_equal(c[f], getattr(S, k), err_msg=f)
+    np.testing.assert_array_equal(be.vec.env.observe().cpu().numpy(), ob.observe(L, S))
+
+
 def test_base_env_absent_agent_does_not_remark_its_cell(wh):
     """Known-answer test of core.py:279-300's dict semantics on co-located agents (Small, 3
     agents; 0 and 1 share cell (2,2), agent 2 at (3,2); action 1 = move -x):
@@ -438,6 +480,45 @@ def test_sampler_step_equals_policy_then_vector_step(wh, variant, na, train, p):
     assert torch.equal(a.state, b.state)
     for k in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
         assert torch.equal(getattr(sa, k), getattr(sb, k)), k
+
+
+@pytest.mark.parametrize("variant,na,train,policy,p,B", [
+    ("medium", 8, False, "greedy", 0.0, 65536), ("medium", 8, False, "greedy", 0.3, 1000),
+    ("large", 16, False, "greedy", 0.0, 777), ("small", 4, True, "greedy", 0.1, 2049),
+    ("medium", 4, False, "random", 0.0, 513), ("large", 16, True, "greedy", 0.0, 300)])
+def test_fused_sampler_step_equals_two_launch_route_and_oracle(wh, variant, na, train, policy, p, B):
+    """wh_sampler_step without episode metrics takes the fused launch (k_sampler: the step on half of
+    each 512-lane workgroup, the rows by all of it, images written from the step's registers).  Its
+    rewards, dones and observation rows equal the two-launch route's (wh_policy + wh_vector_step
+    with auto-reset = step kernel + k_observe) at every step over 210 steps (episode ends, fresh
+    reset rows, a Train variant's new n), full-size and ragged batches (a partial last workgroup);
+    the final states are equal; and a sample of envs equals the oracle's rollout."""
+    import torch
+
+    seed, K = 17, 210
+    L = oc.layout_for(variant)
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    a.reset()
+    b.reset()
+    ids = np.unique(np.r_[np.arange(min(B, 64)), np.linspace(0, B - 1, 64).astype(np.int64)])
+    S = ob.BState.zeros(L, len(ids), na)
+    d = ob.PhiloxDraws(seed, ids)
+    nmax = na if train else None
+    ob.reset(L, S, d, nmax=nmax)
+    for s in range(K):
+        oa, ra, da = a.sampler_step(policy, p)
+        ob_, rb, db = b.vector_step(b.policy(policy, p), autoreset=True)
+        assert torch.equal(ra, rb) and torch.equal(da, db), f"step {s}"
+        assert torch.equal(oa, ob_), f"obs step {s}"
+        acts = ob.greedy(L, S, p, d) if policy == "greedy" else ob.random_actions(S, d)
+        orew, odone, _, _ = ob.step(L, S, acts, d)
+        np.testing.assert_array_equal(ra.cpu().numpy()[ids], orew, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
+        if s % 40 == 0 or s == K - 1:
+            np.testing.assert_array_equal(oa.cpu().numpy()[ids], ob.observe(L, S), err_msg=f"obs step {s}")
+    assert torch.equal(a.state, b.state)
 
 
 @pytest.mark.parametrize("variant,na,train,B", [("medium", 8, False, 4096), ("medium", 9, True, 1000),

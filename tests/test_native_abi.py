@@ -35,14 +35,56 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_library_built_from_this_tree():
-    """Provenance: wh_version() carries the sha of the kernel sources the library was built from
-    (Makefile), equal to the tree's; the assert-mode build carries the same sha."""
+    """Provenance: wh_version() carries the sha of every file the code depends on (kernel sources,
+    version.cpp, the Makefile with its flags, include/warehouse_amd.h) equal to the tree's, and no
+    variant; the assert-mode build carries the same sha and only the WH_CHECK variant."""
     from warehouse import _native
 
     sha = _native.tree_source_sha()
     assert _native.version_sha(_native.lib().wh_version()) == sha
     assert _native.verify_provenance(extra_libs=[os.path.join(ROOT, "build_ab", "check.so")]) == sha
-    assert _native.file_source_sha(_native.LIB_PATH) == sha
+    assert _native.file_version(_native.LIB_PATH) == (sha, "")
+    assert _native.file_version(os.path.join(ROOT, "build_ab", "check.so")) == (sha, _native.CHECK_VARIANT)
+    names = [os.path.basename(p) for p in _native.hashed_files()]
+    assert {"Makefile", "version.cpp", "warehouse_amd.hip", "policy_mlp.hip", "philox.h", "warehouse_amd.h"} <= set(names)
+
+
+def _probe_version(tmp_path, *make_args):
+    """wh_version() of a build with these make settings (the Makefile's version_probe target: g++ on
+    version.cpp only, no kernels compiled)."""
+    import ctypes
+
+    csrc = os.path.join(ROOT, "rllib-warehouse_amd", "csrc")
+    subprocess.run(["make", "-s", "-C", csrc, "version_probe", f"OBJDIR={tmp_path}", *make_args], check=True)
+    L = ctypes.CDLL(os.path.join(str(tmp_path), "version_probe.so"))
+    L.wh_version.restype = ctypes.c_char_p
+    return L.wh_version()
+
+
+def test_variant_build_fails_provenance(tmp_path):
+    """A library built from the same sources but with another -D flag, scheduler or flag set carries
+    a variant tag, and verify_provenance's check refuses it as the production library (the assert-mode
+    tag is accepted only for the extra check.so)."""
+    from warehouse import _native
+
+    sha = _native.tree_source_sha()
+    plain = _probe_version(tmp_path / "plain")
+    assert _native.parse_version(plain) == (sha, "")
+    _native.check_provenance(plain, sha)
+    for k, args in enumerate((["EXTRA=-DWH_ABLATION"], ["EXTRA=-DWH_FORCE_NOREV"], ["SCHED_warehouse_amd=-mllvm -amdgpu-sched-strategy=max-ilp"],
+                 ["FLAGS=--offload-arch=gfx950 -O1"])):
+        v = _probe_version(tmp_path / f"v{k}", *args)   # (a distinct path each: dlopen caches by path)
+        got_sha, variant = _native.parse_version(v)
+        assert got_sha == sha and variant == args[0], v
+        with pytest.raises(_native.WarehouseNativeError, match="variant"):
+            _native.check_provenance(v, sha)
+    chk = _probe_version(tmp_path / "check", "EXTRA=-DWH_CHECK")
+    assert b"assert mode" in chk
+    _native.check_provenance(chk, sha, ("", _native.CHECK_VARIANT))
+    with pytest.raises(_native.WarehouseNativeError, match="variant"):
+        _native.check_provenance(chk, sha)
+    with pytest.raises(_native.WarehouseNativeError, match="stale"):
+        _native.check_provenance(plain, "0" * 16)
 
 
 @pytest.mark.parametrize("variant", ["small", "medium", "large"])

@@ -45,6 +45,59 @@ def test_g1_trajectory(path, mode):
         np.testing.assert_array_equal(oc.observe(L, st), g["obs"][s])
 
 
+KEYS = sorted(glob.glob(os.path.join(GOLDEN, "keys_*.npz")))
+
+
+@pytest.mark.parametrize("path", KEYS, ids=[os.path.basename(p) for p in KEYS])
+@pytest.mark.parametrize("mode", ["injected", "global_mt19937"])
+def test_keys_trajectory(path, mode):
+    """keys_*: dicts keyed by int, negative (numpy wrap) and repeated agents, through the oracle's
+    dict-taking step (OracleWarehouse.step, as core.py:279-281 reads the dict) and through the
+    batched oracle with the C ABI's encoded order entries (agent | (action + 1) << 8)."""
+    from keyforms import encoded_order, key_dict
+    from oracle import batched as ob
+
+    g = np.load(path)
+    L = oc.layout_for(str(g["variant"]))
+    n = int(g["n"])
+    steps = len(g["t"])
+    if mode == "injected":
+        draws = oc.InjectedDraws(spawn=g["spawn"], reset_sel=g["reset_sel"], reset_tgt=g["reset_tgt"],
+                                 regen=[(g["rpos"][s], g["rtgt"][s]) for s in range(steps)])
+    else:
+        np.random.seed(int(g["seed"]))
+        draws = oc.GlobalNumpyDraws()
+    env = oc.OracleWarehouse(str(g["variant"]), n, draws=draws)
+    env.reset()
+    dicts = [key_dict(g["key_form"][s], g["key_agent"][s], g["key_act"][s], n) for s in range(steps)]
+    assert sum(len({int(k) % n for k in d}) < len(d) for d in dicts) > 10      # repeated agents
+    assert sum(any(int(k) < 0 for k in d) for d in dicts) > 10                 # negative keys
+    for s in range(steps):
+        pre_pos = env.state.pos.copy()
+        _, rew, dones, _ = env.step(dicts[s])
+        st = env.state
+        np.testing.assert_array_equal(st.pos, g["pos"][s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(st.pk_tgt, g["pk_tgt"][s])
+        assert [rew[str(i)] for i in range(n)] == list(g["rewards"][s])
+        np.testing.assert_array_equal(oc.observe(L, st), g["obs"][s])
+        # the move phase alone through the batched oracle's encoded order entries
+        pos = pre_pos[None].copy()
+        S = ob.BState.zeros(L, 1, n)
+        S.pos[:] = pos
+        S.n[:] = n
+        order = np.array([encoded_order(dicts[s], n, n)], np.int32)
+        ob_pos = _batched_moves(L, S, order)
+        np.testing.assert_array_equal(ob_pos[0], g["pos"][s], err_msg=f"batched moves, step {s}")
+
+
+def _batched_moves(L, S, order):
+    """Positions after the batched oracle's move phase (the rest of its step is irrelevant here)."""
+    from oracle import batched as ob
+
+    ob.step(L, S, np.full((S.B, S.NA), 4, np.int32), ob.PhiloxDraws(0, np.arange(S.B)), order=order)
+    return S.pos
+
+
 @pytest.mark.parametrize("variant", ["small", "medium", "large"])
 def test_g2_dense_transitions(variant):
     g = np.load(os.path.join(GOLDEN, f"g2_{variant}.npz"))

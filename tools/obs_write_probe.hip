@@ -1,0 +1,108 @@
+// Write-phase probe for a fused sampler kernel (round 4): how fast can a workgroup of THREADS lanes
+// stream the f32 observation rows of ENVS envs (Medium-8: 8 rows x 82 floats per env) gathered from
+// per-env byte images in LDS, as k_observe's write loop does?  Shapes: k_observe's own (256 lanes,
+// 16 envs) against the shapes a fused step + rows kernel would have (512 / 1024 lanes, 256 envs,
+// one workgroup per CU).  MODE 0: gather from LDS (k_observe's loop); MODE 1: the same with the LDS
+// reads of U iterations issued before their stores; MODE 2: stores of a constant (no gathers).
+//   hipcc --offload-arch=gfx950 -O3 tools/obs_write_probe.hip -o tools/obs_write_probe_bin
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+constexpr int NA = 8, L = 82, IMG = 84, PER_ENV = NA * L, QE = PER_ENV / 4;   // 164 float4 per env
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int THREADS, int ENVS, int MODE, int U>
+__global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int64_t B) {
+  __shared__ uint8_t img[ENVS][IMG];
+  __shared__ uint32_t lim[ENVS];
+  __shared__ uint32_t src[QE];
+  const int tid = threadIdx.x;
+  for (int k = tid; k < ENVS * IMG; k += THREADS) (&img[0][0])[k] = (uint8_t)((k * 7) & 31);
+  for (int k = tid; k < ENVS; k += THREADS) lim[k] = PER_ENV - 4 * (k & 3);
+  for (int k = tid; k < QE; k += THREADS) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) w |= (uint32_t)((4 * k + b) % L) << (8 * b);
+    src[k] = w;
+  }
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * ENVS;
+  const uint32_t nenv = (uint32_t)((B - e0) < ENVS ? (B - e0) : ENVS);
+  const uint32_t total = nenv * QE;
+  const uint32_t magic = 0xFFFFFFFFu / QE + 1u;
+  f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * PER_ENV);
+  if (MODE == 2) {
+    for (uint32_t q = tid; q < total; q += THREADS) out4[q] = (f32x4){1.0f, 2.0f, 3.0f, 4.0f};
+    return;
+  }
+  auto value = [&](uint32_t q) -> f32x4 {
+    const uint32_t el4 = __umulhi(q, magic);
+    const uint32_t k4 = q - el4 * QE;
+    const uint32_t lm = lim[el4];
+    const uint32_t sw = src[k4];
+    const int live = (int)lm - 4 * (int)k4;
+    const uint8_t* im = img[el4];
+    f32x4 v;
+    v.x = live > 0 ? (float)im[sw & 0xFFu] : 0.0f;
+    v.y = live > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
+    v.z = live > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
+    v.w = live > 3 ? (float)im[sw >> 24] : 0.0f;
+    return v;
+  };
+  if (MODE == 0) {
+    for (uint32_t q = tid; q < total; q += THREADS) out4[q] = value(q);
+  } else {
+    uint32_t q = tid;
+    for (; q + (U - 1) * THREADS < total; q += U * THREADS) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = value(q + u * THREADS);
+#pragma unroll
+      for (int u = 0; u < U; ++u) out4[q + u * THREADS] = v[u];
+    }
+    for (; q < total; q += THREADS) out4[q] = value(q);
+  }
+}
+
+template <int THREADS, int ENVS, int MODE, int U = 1>
+void run(float* obs, int64_t B, const char* name) {
+  const unsigned grid = (unsigned)((B + ENVS - 1) / ENVS);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(a, 0);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    best = ms / 20 < best ? ms / 20 : best;
+  }
+  const double bytes = (double)B * PER_ENV * 4;
+  printf("%-44s threads=%4d envs/WG=%3d grid=%6u: %7.2f us  %6.2f TB/s\n", name, THREADS, ENVS, grid, best * 1e3,
+         bytes / (best * 1e-3) / 1e12);
+}
+
+int main() {
+  const int64_t B = 65536;
+  float* obs;
+  hipMalloc(&obs, (size_t)B * PER_ENV * 4);
+  run<256, 16, 0>(obs, B, "k_observe shape, gather");
+  run<256, 16, 2>(obs, B, "k_observe shape, constant stores");
+  run<256, 64, 0>(obs, B, "256 lanes 64 envs, gather");
+  run<512, 256, 0>(obs, B, "fused 512 lanes, gather");
+  run<512, 256, 1, 2>(obs, B, "fused 512 lanes, gather unroll 2");
+  run<512, 256, 1, 4>(obs, B, "fused 512 lanes, gather unroll 4");
+  run<512, 256, 2>(obs, B, "fused 512 lanes, constant stores");
+  run<1024, 256, 0>(obs, B, "fused 1024 lanes, gather");
+  run<1024, 256, 1, 2>(obs, B, "fused 1024 lanes, gather unroll 2");
+  run<1024, 256, 2>(obs, B, "fused 1024 lanes, constant stores");
+  run<256, 256, 0>(obs, B, "fused 256 lanes, gather");
+  run<256, 256, 1, 4>(obs, B, "fused 256 lanes, gather unroll 4");
+  run<256, 256, 2>(obs, B, "fused 256 lanes, constant stores");
+  run<512, 128, 0>(obs, B, "512 lanes 128 envs, gather");
+  return 0;
+}
