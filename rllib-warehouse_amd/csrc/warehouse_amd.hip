@@ -1891,10 +1891,11 @@ struct SampLds {
 // k_observe builds from the packed state (n, availability, delivery targets, positions, the open
 // requests in ascending pickup order with their pickup and delivery cells).
 template <class C>
-__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid) {
+__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid, int na) {
   using F = FImg<C::R>;
   uint8_t* im = O.img[tid];
-  const uint32_t n = (s.hdr >> 16) & 0xFFu;
+  uint32_t n = (s.hdr >> 16) & 0xFFu;
+  n = n < (uint32_t)na ? n : (uint32_t)na;
   const bool fresh = (s.hdr >> 24) & 1u;
   constexpr uint32_t nul = (uint32_t)(C::D / 2), nul2 = nul | (nul << 8);
   im[0] = (uint8_t)n;
@@ -1932,7 +1933,11 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
   O.lim[tid] = n * (uint32_t)C::L | (fresh ? 0x80000000u : 0u);
 }
 
-template <class C, int POLICY>
+// FAST: the fused rollout's step (run_steps_fast, greedy/random policy, every env stepped; the
+// wh_sampler_step case).  Otherwise wh_vector_step's: external actions in ascending or action-dict
+// order (ORDERED), an optional env mask -- envs not stepped keep their state and still get their
+// rows -- and the launch options of k_step's generic instance (episode metrics, odd agent counts).
+template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restrict__ obs) {
   __shared__ Lds<C> L;
   __shared__ SampLds<C> O;
@@ -1940,9 +1945,11 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   const bool stepper = tid < BT;
   const int64_t e0 = (int64_t)blockIdx.x * BT;
   const int64_t e = e0 + tid;
-  const bool live = stepper && e < a.B;
+  const bool loaded = stepper && e < a.B;                              // its rows are written
+  const bool stepped = loaded && (FAST || !a.mask || a.mask[e]);       // and it is stepped
+  const int na = FAST ? C::NAM : a.na;
   RawEnv<C> raw;
-  if (live) load_env_issue<C>(raw, a.state, a.B, e, C::NAM);
+  if (loaded) load_env_issue<C>(raw, a.state, a.B, e, na);
   if (stepper) {
     load_tables<C>(L.tbl, a.tables);
   } else {
@@ -1950,26 +1957,31 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
   }
   __syncthreads();
-  if (live) {
+  if (loaded) {
     const Keys k{a.k0, a.k1};
     const uint32_t gid = (uint32_t)(a.env_offset + e);
     Regs<C> s;
     load_env_finish<C>(s, L, raw, (uint32_t)a.W, tid);
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): drain the state loads before the step (k_step)
+    if (stepped) {
 #pragma unroll
-    for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
-    run_steps_fast<C, POLICY, false>(a, s, L, nullptr, k, gid, e, tid);
-    store_env<C>(s, L, a.state, a.B, e, C::NAM, tid);
-    write_image<C>(s, L, O, tid);
+      for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+      if constexpr (FAST)
+        run_steps_fast<C, POLICY, false>(a, s, L, nullptr, k, gid, e, tid);
+      else
+        run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+      store_env<C>(s, L, a.state, a.B, e, na, tid);
+    }
+    write_image<C>(s, L, O, tid, na);
   }
   __syncthreads();
-  // rows of the group's envs: one contiguous [nenv x NA x L] f32 region, float4 per lane (NA * L
+  // rows of the group's envs: one contiguous [nenv x na x L] f32 region, float4 per lane (na * L
   // % 4 == 0 and obs 16-byte aligned: checked on the host)
   const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
-  constexpr uint32_t qe = (uint32_t)(C::NAM * C::L / 4);
-  constexpr uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
+  const uint32_t qe = FAST ? (uint32_t)(C::NAM * C::L / 4) : (uint32_t)(na * C::L / 4);
+  const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
   const uint32_t total = nenv * qe;
-  f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * (int64_t)(C::NAM * C::L));
+  f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * (int64_t)(4 * qe));
   for (uint32_t q = tid; q < total; q += 2 * BT) {
     const uint32_t el4 = __umulhi(q, magic);
     const uint32_t k4 = q - el4 * qe;
@@ -2208,6 +2220,7 @@ struct Kernels {
   void (*step_fast[3])(StepParams);   // [policy]: greedy / random fused rollouts (NAM even), else null
   void (*step_ordered)(StepParams);
   void (*sampler[3])(StepParams, float*);   // [policy]: fused step + rows (k_sampler), NAM even, else null
+  void (*vsampler[2])(StepParams, float*);  // [ordered]: wh_vector_step's step + rows (external actions)
   void (*reset)(ResetParams);
   void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // 8 / 16 / 64 envs per WG
   int tblw, nv;
@@ -2226,13 +2239,15 @@ Kernels make_kernels() {
   if constexpr (NAM % 2 == 0) {
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
-    k.sampler[1] = k_sampler<C, POL_GREEDY>;
-    k.sampler[2] = k_sampler<C, POL_RANDOM>;
+    k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
+    k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
   } else {
     k.step_fast[1] = k.step_fast[2] = nullptr;
     k.sampler[1] = k.sampler[2] = nullptr;
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
+  k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
+  k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
   k.observe[0] = k_observe<C, 8>;
   k.observe[1] = k_observe<C, 16>;
@@ -2260,6 +2275,21 @@ const std::vector<Kernels>& registry() {
   };
 #endif
   return r;
+}
+
+// A fused step + rows kernel (k_sampler) runs two waves per SIMD, so its step code gets 256
+// registers instead of 512: configurations whose step needs more spill to scratch there (Large-16)
+// and keep the two launches.  Decided once per kernel from its private segment size.
+bool fused_ok(void (*kern)(StepParams, float*)) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, bool>> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const auto& p : seen)
+    if (p.first == reinterpret_cast<const void*>(kern)) return p.second;
+  hipFuncAttributes at;
+  const bool ok = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(kern)) == hipSuccess && at.localSizeBytes == 0;
+  seen.emplace_back(reinterpret_cast<const void*>(kern), ok);
+  return ok;
 }
 
 const Kernels* pick(const Geometry& g) {
@@ -2623,7 +2653,23 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
   a.autoreset = autoreset ? 1 : 0;
   a.variable_n = variable_n ? 1 : 0;
   if (stats) a.stats = *stats;
-  int rc = launch_step(cfg, B, state, POL_EXTERNAL, a, stream);
+  wh_launch l;
+  int rc = resolve_step(cfg, B, state, POL_EXTERNAL, a, stream, &l);
+  if (rc) return rc;
+  // one launch (k_sampler's generic instance: the step on half of each workgroup, every env's rows
+  // by all of it) when its step code keeps its registers and the rows are whole float4s
+  static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
+  Geometry g;
+  const Kernels* k = nullptr;
+  const uint32_t* tab = nullptr;
+  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK) {
+    void (*fk)(StepParams, float*) = k->vsampler[order ? 1 : 0];
+    if (fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+      hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
+      return hip_err(hipGetLastError());
+    }
+  }
+  rc = enqueue(l);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
 }
@@ -2656,7 +2702,7 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
   const Kernels* k = nullptr;
   const uint32_t* tab = nullptr;
   if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && l.kern == k->step_fast[policy] &&
-      k->sampler[policy] && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+      k->sampler[policy] && fused_ok(k->sampler[policy]) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
     hipLaunchKernelGGL(k->sampler[policy], grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
     return hip_err(hipGetLastError());
   }

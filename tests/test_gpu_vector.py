@@ -521,6 +521,47 @@ def test_fused_sampler_step_equals_two_launch_route_and_oracle(wh, variant, na, 
     assert torch.equal(a.state, b.state)
 
 
+@pytest.mark.parametrize("variant,na,train,B,masked,ordered,stats", [
+    ("medium", 8, False, 65536, False, False, False), ("medium", 8, False, 1000, True, True, True),
+    ("small", 4, True, 2049, True, False, True), ("medium", 4, False, 513, False, True, False),
+    ("medium", 2, False, 300, True, True, False)])
+def test_fused_vector_step_equals_two_launch_route(wh, variant, na, train, B, masked, ordered, stats):
+    """wh_vector_step with observation rows takes one launch (k_sampler's generic instance: external
+    actions, optional env mask and action-dict order, episode metrics) where its step code keeps its
+    registers; it must equal the two launches it replaces -- the step alone (observe=False) then
+    wh_observe -- in rewards, dones (stepped envs), rows of EVERY env (masked-out envs keep theirs),
+    episode metrics and state, over 210 steps with auto-reset."""
+    import torch
+
+    seed, K = 23, 210
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    if stats:
+        sa, sb = a.enable_episode_stats(), b.enable_episode_stats()
+    a.reset()
+    b.reset()
+    NA = a.agent_slots
+    rng = np.random.default_rng(5)
+    for s in range(K):
+        acts = torch.from_numpy(rng.integers(0, 9, (B, NA), dtype=np.int32))
+        mask = torch.from_numpy(rng.random(B) < 0.6) if masked and s % 2 else None
+        order = None
+        if ordered and s % 3:
+            perm = np.argsort(rng.random((B, NA)), axis=1).astype(np.int32)
+            drop = rng.random((B, NA)) < 0.2
+            order = torch.from_numpy(np.where(np.cumsum(drop, axis=1) > 0, -1, perm).astype(np.int32))
+        oa, ra, da = a.vector_step(acts, autoreset=True, mask=mask, order=order)
+        _, rb, db = b.vector_step(acts, autoreset=True, mask=mask, order=order, observe=False)
+        ob_ = b.observe()
+        live = slice(None) if mask is None else mask.to(ra.device)
+        assert torch.equal(ra[live], rb[live]) and torch.equal(da[live], db[live]), f"step {s}"
+        assert torch.equal(oa, ob_), f"obs step {s}"
+    assert torch.equal(a.state, b.state)
+    if stats:
+        for k in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
+            assert torch.equal(getattr(sa, k), getattr(sb, k)), k
+
+
 @pytest.mark.parametrize("variant,na,train,B", [("medium", 8, False, 4096), ("medium", 9, True, 1000),
                                                 ("large", 16, False, 777), ("large", 5, False, 300),
                                                 ("small", 4, True, 2049), ("small", 3, False, 129)])

@@ -9,7 +9,8 @@ import re
 import sys
 
 SYM = next((a for a in sys.argv[1:] if not a.startswith("-")), None) or "k_stepINS_3CfgILi16ELi9ELi3ELi8EEELi1ELb0ELb1EE"
-lines = open("rllib-warehouse_amd/csrc/warehouse_amd.s").read().splitlines()
+import os
+lines = open(os.environ.get("WH_ASM", "rllib-warehouse_amd/csrc/warehouse_amd.s")).read().splitlines()
 start = next(i for i, l in enumerate(lines) if l.startswith("_ZN") and SYM in l and l.split(";")[0].rstrip().endswith(":"))
 end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
 phase = "prologue"
