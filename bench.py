@@ -368,6 +368,42 @@ def measure_sampler(env, K, W, dev, world, dist):
     return elapsed, split
 
 
+def measure_sampler_rollout(env, K, frag, W, dev, world, dist):
+    """The sampler route as rollout fragments (wh_sampler_rollout): `frag` sampler steps per launch,
+    the obs rows / rewards / dones of every step kept ([frag,B,NA,9R+1] ...), K steps in the timed
+    window.  Returns (elapsed_s, ms per launch timed alone between HIP events)."""
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+    B, NA = env.B, env.agent_slots
+    obs = torch.empty((frag, B, NA, env.obs_len), device=dev)
+    rew = torch.empty((frag, B, NA), device=dev)
+    dn = torch.empty((frag, B), dtype=torch.uint8, device=dev)
+
+    def one():
+        env.sampler_rollout(frag, "greedy", 0.0, obs=obs, rewards=rew, dones=dn)
+
+    for _ in range(max(W // frag, 2)):
+        one()
+    torch.cuda.synchronize(dev)
+    n = max(1, K // frag)
+
+    def run():
+        for _ in range(n):
+            one()
+
+    elapsed = timed_window(run, lambda: torch.cuda.synchronize(dev), world, dist)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a, b in evs:
+        a.record(stream)
+        one()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kms = sorted(a.elapsed_time(b) for a, b in evs)
+    del obs
+    return elapsed, n * frag, kms[len(kms) // 2]
+
+
 def measure_vector(env, K, W, dev, world, dist):
     """The RLlib route with the learner's actions (scripts/train.py's MultiAgentEnv sampler, through
     WarehouseVectorEnv): per step wh_vector_step = external actions [B,NA] -> step + auto-reset +
@@ -665,6 +701,23 @@ def main():
                          "note": "algorithmic bytes = B*NA*(9R+1)*4 rows + 2 x packed state + rewards + dones"},
         }
 
+    fragment = None
+    if not args.no_sampler:
+        frag = 20
+        el7, Kf, fms2 = measure_sampler_rollout(env, max(min(K, 1000), 200), frag, W, dev, world, dist)
+        frag_b = frag * (B * NA * env.obs_len * 4 + B * (4 * NA + 1)) + 2 * B * 4 * words
+        fragment = {
+            "workload": f"the sampler route as rollout fragments: wh_sampler_rollout = {frag} sampler steps (device greedy "
+                        f"policy + step + auto-reset + f32 observation rows) per launch, every step's rows kept "
+                        f"([{frag},B,{NA},{env.obs_len}]); {Kf} steps timed",
+            "value": aggregate_rate(world, B, NA, Kf, el7), "unit": "agent-steps/s", "steps": Kf,
+            "ms_per_step": el7 * 1e3 / Kf,
+            "roofline": {"bound": "hbm", "kernel": f"k_sampler ({frag} steps per launch)", "kernel_ms": fms2,
+                         "bytes_per_launch": frag_b, "achieved": frag_b / (fms2 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": frag_b / (fms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "algorithmic bytes = per step rows + rewards + dones, + 2 x packed state per launch"},
+        }
+
     vector = None
     if not args.no_sampler:
         Kv = max(min(K, 1000), 200)
@@ -742,6 +795,7 @@ def main():
             "alt_launch_mode": alt,
             "desync_episodes": desync,
             "sampler_path": sampler,
+            "sampler_fragments": fragment,
             "vector_path": vector,
             "policy_path": policy_line,
             "policy_path_f32": policy_f32,

@@ -194,6 +194,15 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
                     float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats,
                     int32_t variable_n, uint64_t seed, int64_t env_offset, void* stream);
 
+/* `steps` consecutive wh_sampler_step's in ONE launch (a rollout fragment of the sampler route):
+ * rewards [steps,B,NA] / dones [steps,B] / obs [steps,B,NA,9R+1] (obs required), step k's outputs at
+ * index k; the same draws, transitions and rows as `steps` calls of wh_sampler_step.  In the fused
+ * launch the simulation of step k runs while step k-1's rows stream out, the state staying in
+ * registers; configurations it does not cover run the steps one call at a time. */
+int wh_sampler_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy, float p,
+                       float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats, int32_t variable_n,
+                       uint64_t seed, int64_t env_offset, void* stream);
+
 /* wh_sampler_step's step launch with the state double-buffered and no observation rows: reads
  * state_in, writes the stepped state to state_out (a distinct [words, B] buffer, or state_in itself).
  * With two state buffers, wh_observe of step s (reading its output buffer) can run on another stream

@@ -1496,8 +1496,77 @@ __device__ __forceinline__ void store_row(float* row, const float (&rew)[C::NAM]
   }
 }
 
-// SLOTS = false (the fused sampler step, k_sampler: one step per launch): no reset slots -- a lone
-// ending lane is reset by reset_lane, as the 1-step launches of k_step do (kSlotMinSteps).
+// One step of the fused rollout's common case at a time (run_steps_fast loops over it; k_sampler
+// interleaves it with writing observation rows).  Carries the lazy grid and the output rows.
+// SLOTS = false: no reset slots -- a lone ending lane is reset by reset_lane, as launches shorter
+// than kSlotMinSteps do.
+template <class C, int POLICY, bool SLOTS = true>
+struct FastRun {
+  float* rrow;
+  uint8_t* drow;
+  int64_t rstride;
+  LazyGrid lg;
+  __device__ __forceinline__ FastRun(const StepParams& a, int64_t e)
+      : rrow(a.rewards + e * C::NAM), drow(a.dones + e), rstride(a.B * C::NAM), lg{true, 0u} {}   // the grid starts empty (k_step)
+
+  __device__ __forceinline__ void step(const StepParams& a, Regs<C>& s, Lds<C>& L, Slots<C>* RS, const Keys& k,
+                                       uint32_t gid, int64_t e, int tid, int stp) {
+#ifdef WH_ABLATION
+    const int ablate = a.ablate;
+#else
+    constexpr int ablate = 0;
+#endif
+    uint32_t d[C::NAM];
+    if (ablate & 1) {
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
+    } else {
+      policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
+    }
+    float rew[C::NAM];
+    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg);
+    if (!(ablate & 64)) {
+      store_row<C>(rrow, rew);
+      *drow = done ? 1 : 0;
+    }
+    rrow += rstride;
+    drow += a.B;
+    if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
+      const uint64_t dm = __ballot(done);
+      // a few envs of a full wave end (desynchronised episodes): wave-wide resets of them, one env
+      // at a time (every lane takes part, so not in a tail wave whose lanes past B have exited)
+      const bool full = __ballot(true) == ~0ull;
+#ifndef WH_NO_RESET_SLOTS   // (A/B builds: -DWH_NO_RESET_SLOTS resets one lane from scratch)
+      if (SLOTS && a.steps >= kSlotMinSteps && __popcll(dm) <= kSlotResetMax && full) {
+        // their precomputed next-episode states, after (re)filling the wave's slots if one of
+        // theirs is stale: one wave-wide fill (every lane's next episode) serves the resets of
+        // the lanes that end later in this launch
+        if constexpr (SLOTS) {
+          if (__any(done && RS->rs_ep[tid] != s.epi + 1u))
+            reset_philox<C, C::NAM, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid, RS);
+          for (uint64_t m = dm; m; m &= m - 1ull) reset_from_slot<C, C::NAM>(s, L, *RS, (uint32_t)a.W, tid, __builtin_ctzll(m));
+          lg.rebuild = lg.rebuild || done;   // their grid columns were cleared
+        }
+      } else
+#endif
+      if (__popcll(dm) == 1 && full) {
+        // short launches (the sampler's 1-step ones): a fill would serve few later resets
+        reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
+        lg.rebuild = lg.rebuild || done;   // its grid column was cleared
+      } else if (done) {
+        reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+#pragma unroll
+        for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
+        lg.rebuild = true;
+      }
+    }
+    WH_CHECK_ENV(s, L, e, tid);
+  }
+};
+
+// k_step's fused rollout loop: FastRun's step, written out as one loop (the same body as a member
+// call measured 2 % slower per step at Medium-8: profiles/r04_fastrun_ab.txt).
 template <class C, int POLICY, bool SLOTS = true>
 __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, Lds<C>& L, Slots<C>* RS,
                                                const Keys& k, uint32_t gid, int64_t e, int tid) {
@@ -1559,6 +1628,7 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
     WH_CHECK_ENV(s, L, e, tid);
   }
 }
+
 
 // -DWH_TIMING builds (tools/launch_timeline.py): per-wave s_memrealtime stamps (100 MHz) of the fused
 // rollout's phases -- entry, tables in LDS, state loaded, step loop done, state stored -- read back
@@ -1882,18 +1952,21 @@ __constant__ ObsSrc<R, NAM> kObsSrcF =
 template <class C>
 struct SampLds {
   static constexpr int IMG = FImg<C::R>::IMG, SRCW = ObsSrc<C::R, C::NAM>::W;
-  alignas(16) uint8_t img[BT][IMG];
-  uint32_t lim[BT];        // n * L (floats of live rows) | fresh << 31
+  // two image buffers: step k's images are written while step k-1's rows stream from the other
+  alignas(16) uint8_t img[2][BT][IMG];
+  uint32_t lim[2][BT];     // n * L (floats of live rows) | fresh << 31
   uint32_t src[2][SRCW];
+  uint32_t next[2];        // row chunks handed out (write_rows), per image buffer
 };
 
 // core.py:224-260 / 371-432 for the env of this lane, from its registers after the step: the image
 // k_observe builds from the packed state (n, availability, delivery targets, positions, the open
 // requests in ascending pickup order with their pickup and delivery cells).
 template <class C>
-__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid, int na) {
+__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid, int na,
+                                            int buf) {
   using F = FImg<C::R>;
-  uint8_t* im = O.img[tid];
+  uint8_t* im = O.img[buf][tid];
   uint32_t n = (s.hdr >> 16) & 0xFFu;
   n = n < (uint32_t)na ? n : (uint32_t)na;
   const bool fresh = (s.hdr >> 24) & 1u;
@@ -1930,17 +2003,71 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
     mlo = (uint32_t)m;
     mhi = (uint32_t)(m >> 32);
   }
-  O.lim[tid] = n * (uint32_t)C::L | (fresh ? 0x80000000u : 0u);
+  O.lim[buf][tid] = n * (uint32_t)C::L | (fresh ? 0x80000000u : 0u);
 }
 
-// FAST: the fused rollout's step (run_steps_fast, greedy/random policy, every env stepped; the
-// wh_sampler_step case).  Otherwise wh_vector_step's: external actions in ascending or action-dict
-// order (ORDERED), an optional env mask -- envs not stepped keep their state and still get their
-// rows -- and the launch options of k_step's generic instance (episode metrics, odd agent counts).
+// Rows of the workgroup's envs from image buffer `buf`: one contiguous [nenv x na x L] f32 region at
+// `rows` (its first env's first float), float4 per lane (na * L % 4 == 0 and 16-byte alignment:
+// checked on the host).  The region is handed out in chunks of kRowChunk float4s from a counter in
+// LDS (O.next[buf], zero on entry), one chunk per wave at a time, so waves that join late (the step
+// lanes, after their step) take what is left instead of a fixed share.
+constexpr uint32_t kRowChunk = 1024;
+template <class C>
+__device__ __forceinline__ void write_rows(SampLds<C>& O, int buf, float* __restrict__ rows, uint32_t nenv,
+                                           uint32_t qe, int tid) {
+  const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
+  const uint32_t total = nenv * qe;
+  const uint32_t lane = (uint32_t)tid & 63u;
+  f32x4* out4 = reinterpret_cast<f32x4*>(rows);
+#ifdef WH_ROWS_STATIC   // (A/B builds: a fixed share per lane, q = tid + 2 BT i)
+  for (uint32_t q0 = (uint32_t)tid - lane; q0 < total; q0 += 2 * BT) {
+    {
+      const uint32_t q = q0 + lane;
+      if (q < total) {
+#else
+  for (;;) {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&O.next[buf], 1u);
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(c) * kRowChunk;
+    if (q0 >= total) break;
+#pragma unroll 4
+    for (uint32_t u = 0; u < kRowChunk; u += 64) {
+      const uint32_t q = q0 + u + lane;
+      if (q < total) {
+#endif
+        const uint32_t el4 = __umulhi(q, magic);
+        const uint32_t k4 = q - el4 * qe;
+        const uint32_t lim = O.lim[buf][el4];
+        const uint32_t sw = O.src[lim >> 31][k4];
+        const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
+        const uint8_t* im = O.img[buf][el4];
+        f32x4 v;
+        v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
+        v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
+        v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
+        v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
+        out4[q] = v;
+      }
+    }
+  }
+}
+
+// FAST: the fused rollout's steps (greedy/random policy, every env stepped, auto-reset): a.steps of
+// them in one launch (wh_sampler_step: 1; wh_sampler_rollout: a rollout fragment), step k's rows
+// going to obs + k * B * NA * L.  Iteration k of the launch loop: the step lanes compute step k and
+// write its images into buffer k % 2 while the other lanes (and the step lanes, once done) stream
+// step k-1's rows from buffer (k-1) % 2; one barrier per iteration.  So after the first step the
+// simulation runs under the row stream, which is what binds (HBM writes).  State stays in registers
+// across the steps, as in the fused rollout (reset slots from 8 steps on).
+// Otherwise (FAST = false) wh_vector_step's single step: external actions in ascending or
+// action-dict order (ORDERED), an optional env mask -- envs not stepped keep their state and still
+// get their rows -- and the launch options of k_step's generic instance (episode metrics, odd agent
+// counts).
 template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restrict__ obs) {
   __shared__ Lds<C> L;
   __shared__ SampLds<C> O;
+  __shared__ std::conditional_t<FAST, Slots<C>, NoSlots> RS;   // reset slots: multi-step launches
   const int tid = threadIdx.x;
   const bool stepper = tid < BT;
   const int64_t e0 = (int64_t)blockIdx.x * BT;
@@ -1955,46 +2082,46 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   } else {
     const uint32_t* srcg = &kObsSrcF<C::R, C::NAM>.w[0][0];
     for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
+    if (tid - BT < 2) O.next[tid - BT] = 0u;
   }
   __syncthreads();
+  const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
+  const uint32_t qe = FAST ? (uint32_t)(C::NAM * C::L / 4) : (uint32_t)(na * C::L / 4);
+  const Keys k{a.k0, a.k1};
+  const uint32_t gid = (uint32_t)(a.env_offset + e);
+  Regs<C> s;
   if (loaded) {
-    const Keys k{a.k0, a.k1};
-    const uint32_t gid = (uint32_t)(a.env_offset + e);
-    Regs<C> s;
     load_env_finish<C>(s, L, raw, (uint32_t)a.W, tid);
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): drain the state loads before the step (k_step)
     if (stepped) {
 #pragma unroll
       for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
-      if constexpr (FAST)
-        run_steps_fast<C, POLICY, false>(a, s, L, nullptr, k, gid, e, tid);
-      else
-        run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+    }
+  }
+  if constexpr (FAST) {
+    if (loaded) RS.rs_ep[tid] = s.epi;   // reset slots start stale (!= epi + 1)
+    FastRun<C, POLICY, true> run(a, e);
+    const int64_t step_floats = a.B * (int64_t)(C::NAM * C::L);
+    for (int it = 0; it <= a.steps; ++it) {   // (every wave reaches every barrier)
+      // iteration it streams buffer (it-1)%2 with counter next[(it-1)%2]; the counter iteration
+      // it+1 uses was last used in iteration it-1, whose readers all passed the barrier before this
+      if (tid == BT && it > 0) O.next[it & 1] = 0u;
+      if (loaded && it < a.steps) {
+        run.step(a, s, L, &RS, k, gid, e, tid, it);
+        write_image<C>(s, L, O, tid, C::NAM, it & 1);
+      }
+      if (it > 0) write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+      __syncthreads();
+    }
+    if (loaded) store_env<C>(s, L, a.state, a.B, e, na, tid);
+  } else {
+    if (stepped) {
+      run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
       store_env<C>(s, L, a.state, a.B, e, na, tid);
     }
-    write_image<C>(s, L, O, tid, na);
-  }
-  __syncthreads();
-  // rows of the group's envs: one contiguous [nenv x na x L] f32 region, float4 per lane (na * L
-  // % 4 == 0 and obs 16-byte aligned: checked on the host)
-  const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
-  const uint32_t qe = FAST ? (uint32_t)(C::NAM * C::L / 4) : (uint32_t)(na * C::L / 4);
-  const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
-  const uint32_t total = nenv * qe;
-  f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * (int64_t)(4 * qe));
-  for (uint32_t q = tid; q < total; q += 2 * BT) {
-    const uint32_t el4 = __umulhi(q, magic);
-    const uint32_t k4 = q - el4 * qe;
-    const uint32_t lim = O.lim[el4];
-    const uint32_t sw = O.src[lim >> 31][k4];
-    const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
-    const uint8_t* im = O.img[el4];
-    f32x4 v;
-    v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
-    v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
-    v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
-    v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
-    out4[q] = v;
+    if (loaded) write_image<C>(s, L, O, tid, na, 0);
+    __syncthreads();
+    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   }
 }
 
@@ -2235,15 +2362,18 @@ Kernels make_kernels() {
   k.step[1] = k_step<C, POL_GREEDY, false, false>;
   k.step[2] = k_step<C, POL_RANDOM, false, false>;
   k.step_fast[0] = nullptr;
-  k.sampler[0] = nullptr;
+  k.sampler[0] = k.sampler[1] = k.sampler[2] = nullptr;
+  // the multi-step sampler holds the step's LDS, its reset slots and two image buffers
+  constexpr bool sampler_fits = sizeof(Lds<C>) + sizeof(Slots<C>) + sizeof(SampLds<C>) <= 160 * 1024;
   if constexpr (NAM % 2 == 0) {
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
-    k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
-    k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
+    if constexpr (sampler_fits) {
+      k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
+      k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
+    }
   } else {
     k.step_fast[1] = k.step_fast[2] = nullptr;
-    k.sampler[1] = k.sampler[2] = nullptr;
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
   k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
@@ -2709,6 +2839,46 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
   rc = enqueue(l);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
+}
+
+int wh_sampler_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, int32_t policy, float p,
+                       float* rewards, uint8_t* dones, float* obs, const wh_episode_stats* stats, int32_t variable_n,
+                       uint64_t seed, int64_t env_offset, void* stream) {
+  if (policy != WH_POLICY_GREEDY && policy != WH_POLICY_RANDOM) return WH_EINVAL;
+  if (steps < 0 || !(p >= 0.0f && p <= 1.0f) || !stats_ok(stats)) return WH_EINVAL;
+  if (B > 0 && steps > 0 && !obs) return WH_EINVAL;
+  StepParams a{};
+  if (stats) a.stats = *stats;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.p = p;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = steps;
+  a.phase = PH_ALL;
+  a.autoreset = 1;
+  a.variable_n = variable_n ? 1 : 0;
+  wh_launch l;
+  int rc = resolve_step(cfg, B, state, policy, a, stream, &l);
+  if (rc || B == 0 || steps == 0) return rc;
+  Geometry g;
+  const Kernels* k = nullptr;
+  const uint32_t* tab = nullptr;
+  if ((rc = prepare(cfg, B, stream, &g, &k, &tab)) != WH_OK) return rc;
+  static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
+  if (!unfused && l.kern == k->step_fast[policy] && k->sampler[policy] && fused_ok(k->sampler[policy]) &&
+      (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+    hipLaunchKernelGGL(k->sampler[policy], grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
+    return hip_err(hipGetLastError());
+  }
+  // otherwise: the same steps one launch (pair) at a time
+  const int64_t rows = B * (int64_t)g.NA * (9 * g.R + 1);
+  for (int32_t t = 0; t < steps && rc == WH_OK; ++t)
+    rc = wh_sampler_step(cfg, B, state, policy, p, rewards ? rewards + (int64_t)t * B * g.NA : nullptr,
+                         dones ? dones + (int64_t)t * B : nullptr, obs + (int64_t)t * rows, stats, variable_n, seed,
+                         env_offset, stream);
+  return rc;
 }
 
 int wh_sampler_step_to(const wh_config* cfg, int64_t B, const uint32_t* state_in, uint32_t* state_out,

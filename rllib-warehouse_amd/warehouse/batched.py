@@ -261,6 +261,27 @@ class BatchedWarehouse:
                    self.env_offset, self.stream)
         return obs, self.rewards, self.dones
 
+    def sampler_rollout(self, steps: int, policy: str = "greedy", p: float = 0.0, obs=None, rewards=None,
+                        dones=None):
+        """`steps` sampler_step's in one launch (wh_sampler_rollout: a rollout fragment): obs
+        [steps,B,NA,9R+1] f32, rewards [steps,B,NA] f32, dones [steps,B] uint8, step k at index k
+        (allocated when None).  Returns (obs, rewards, dones)."""
+        NA, L = self.agent_slots, self.obs_len
+        shapes = ((steps, self.B, NA, L), (steps, self.B, NA), (steps, self.B))
+        dt = (torch.float32, torch.float32, torch.uint8)
+        out = []
+        for t, shape, d in zip((obs, rewards, dones), shapes, dt):
+            if t is None:
+                t = torch.empty(shape, dtype=d, device=self.device)
+            elif tuple(t.shape) != shape:
+                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+            out.append(t)
+        self._call("wh_sampler_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
+                   nat.ptr(out[1]), nat.ptr(out[2]), nat.ptr(out[0]),
+                   None if self.stats is None else self.stats.ref, int(self.train), self.seed, self.env_offset,
+                   self.stream)
+        return tuple(out)
+
     def policy(self, kind: str = "greedy", p: float = 0.0) -> torch.Tensor:
         self._call("wh_policy", self.state.data_ptr(), POLICIES[kind], float(p), self.actions.data_ptr(),
                    self.seed, self.env_offset, self.stream)

@@ -521,6 +521,60 @@ def test_fused_sampler_step_equals_two_launch_route_and_oracle(wh, variant, na, 
     assert torch.equal(a.state, b.state)
 
 
+@pytest.mark.parametrize("variant,na,train,policy,p,B,K,stagger,stats", [
+    ("medium", 8, False, "greedy", 0.0, 65536, 24, False, False), ("medium", 8, False, "greedy", 0.0, 4096, 40, True, False),
+    ("medium", 8, False, "greedy", 0.3, 1000, 7, True, False), ("small", 4, True, "greedy", 0.1, 2049, 12, False, False),
+    ("medium", 4, False, "random", 0.0, 513, 9, False, False), ("large", 16, False, "greedy", 0.0, 777, 10, True, False),
+    ("medium", 8, False, "greedy", 0.0, 300, 5, False, True)])
+def test_sampler_rollout_equals_sampler_steps(wh, variant, na, train, policy, p, B, K, stagger, stats):
+    """wh_sampler_rollout (K sampler steps in one launch: the simulation of step k under the row stream
+    of step k-1, state in registers, reset slots from 8 steps on) == K calls of wh_sampler_step:
+    rewards, dones and observation rows of every step, episode metrics and the final state; launches
+    across episode ends with desynchronised episodes (several lanes of a wave ending on one step),
+    Train variants, p > 0, random actions, ragged batches; configurations outside the fused kernel
+    (Large-16: the step would spill at two waves per SIMD; episode metrics) take the per-step path.
+    A sample of envs equals the oracle."""
+    import torch
+
+    seed = 29
+    L = oc.layout_for(variant)
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=seed)
+    if stats:
+        sa, sb = a.enable_episode_stats(), b.enable_episode_stats()
+    a.reset()
+    b.reset()
+    if stagger:
+        off = (np.arange(B, dtype=np.int64) * 37) % 200
+        a.stagger(off, policy, p)
+        b.stagger(off, policy, p)
+    ids = np.unique(np.linspace(0, B - 1, 48).astype(np.int64))
+    c0 = {kk: v.cpu().numpy()[ids] for kk, v in a.to_canonical().items()}
+    for rep in range(2):   # two launches back to back (the second starts from the first's state)
+        obs, rew, dn = a.sampler_rollout(K, policy, p)
+        for t in range(K):
+            ob_, rb, db = b.sampler_step(policy, p)
+            assert torch.equal(rew[t], rb) and torch.equal(dn[t], db), f"launch {rep} step {t}"
+            assert torch.equal(obs[t], ob_), f"obs launch {rep} step {t}"
+    assert torch.equal(a.state, b.state)
+    if stats:
+        for kk in ("return_sum", "episodes", "return_min", "return_max", "episode_return"):
+            assert torch.equal(getattr(sa, kk), getattr(sb, kk)), kk
+    # the last launch's final rows for a sample of envs against the oracle, from their start state
+    S = ob.BState(pos=c0["pos"].copy(), agent_tgt=c0["agent_target"].copy(), pk_tgt=c0["pickup_target"].copy(),
+                  pk_timer=c0["pickup_timer"].copy(), t=c0["t"].astype(np.int64), n=c0["n"].copy(),
+                  fresh=c0["fresh"].astype(bool), episode=c0["episode"].astype(np.uint32))
+    d = ob.PhiloxDraws(seed, ids)
+    nmax = a.agent_slots if train else None
+    for t in range(2 * K):
+        acts = ob.greedy(L, S, p, d) if policy == "greedy" else ob.random_actions(S, d)
+        orew, odone, _, _ = ob.step(L, S, acts, d)
+        if odone.any():
+            ob.reset(L, S, d, mask=odone, nmax=nmax)
+    np.testing.assert_array_equal(obs[K - 1].cpu().numpy()[ids], ob.observe(L, S))
+    np.testing.assert_array_equal(rew[K - 1].cpu().numpy()[ids], orew)
+
+
 @pytest.mark.parametrize("variant,na,train,B,masked,ordered,stats", [
     ("medium", 8, False, 65536, False, False, False), ("medium", 8, False, 1000, True, True, True),
     ("small", 4, True, 2049, True, False, True), ("medium", 4, False, 513, False, True, False),
