@@ -448,6 +448,276 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------ bf16 on 16x16x32 tiles
+// The same network and dataflows on v_mfma_f32_16x16x32_bf16 (k_mlp16, the default).  On gfx950 a
+// loop of this shape holds a higher clock under load than the 32x32x16 loop at equal cycles per FLOP
+// (MI355X_MICROARCH.md, 'DVFS give-back' item 7: 1.12-1.14x FLOP/s with the operands re-read from
+// LDS), and its accumulator is 4 registers instead of 16.  Layouts (cdna_hip_programming.md §3):
+// A lane l = row l&15, k 8(l>>4)+j; B lane l = column l&15, same k; C lane l = column l&15, rows
+// 4(l>>4)+i.  A wave still computes 32 samples: two sample tiles s of 16 columns, each staged A
+// fragment (16 hidden rows x 32 k, 1 KiB) feeding one MFMA per sample tile.  Hidden units come in
+// groups of 32 = two 16-row tiles whose accumulators, bias + ReLU + bf16, are register for register
+// the B fragment of one 32-k step of the next layer: element j of lane l is unit
+// 32m + (j < 4 ? 4g + j : 16 + 4g + j - 4), g = l>>4 (kperm16, folded into the packed weights).
+//  MODE 0: layer 0 group by group (all H0 units kept as B fragments, 2 x 4 VGPRs per group), then
+//    layer 1 group by group with K = H0 at hand, each group's two tiles feeding one W2 k-step.
+//  MODE 1 (Large): all layer-1 tiles live (2 x 4 VGPRs each); layer-0 groups streamed through them.
+template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_>
+struct Net16 {
+  static constexpr int IN = IN_, INP = (IN_ + 2 + 31) / 32 * 32, H0 = H0_, H1 = H1_, OUT = 9;
+  static constexpr int KQ0 = INP / 32;              // layer-0 k-steps of 32
+  static constexpr int KQX = (IN_ + 2 + 15) / 16;   // k-steps of 16 in wh_observe_x's operand
+  static constexpr int G0 = H0 / 32, G1 = H1 / 32;  // groups of 32 hidden units
+  static constexpr int WAVES = WAVES_, MT = 64 * WAVES_, ROWS = 32 * WAVES_;
+  static constexpr int MODE = MODE_, L0T = L0T_, L1T = L1T_;
+  static constexpr int U0 = MODE == 0 ? 2 * KQ0 : 2 * KQ0 + 2 * G1;   // operands per layer-0 group
+  static constexpr int U1 = 2 * G0 + 1;                               // MODE 0: per layer-1 group (+ W2)
+  static constexpr int L0C = G0 / L0T, L0OPS = L0T * U0;
+  static constexpr int L1C = MODE == 0 ? G1 / L1T : 1, L1OPS = MODE == 0 ? L1T * U1 : G1;
+  static constexpr int NCH = L0C + L1C;
+  static constexpr int SOPS = L0OPS > L1OPS ? L0OPS : L1OPS;
+  static constexpr int64_t STREAM_OPS = (int64_t)L0C * L0OPS + (int64_t)L1C * L1OPS;
+  static constexpr int64_t BIAS_OFF = STREAM_OPS * 1024;
+  static constexpr int64_t BYTES = BIAS_OFF + 4 * (H0 + H1 + 32);
+  static constexpr int STAGES = 2;
+  static constexpr int LDS_BYTES = STAGES * SOPS * 1024 + 4 * H1;
+  static_assert(H0 % 32 == 0 && H1 % 32 == 0 && G0 % L0T == 0 && (MODE == 1 || G1 % L1T == 0), "tile shapes");
+  static_assert(LDS_BYTES <= 160 * 1024, "two weight stages + b1 must fit the 160 KiB LDS");
+  __host__ __device__ static constexpr int64_t chunk_off(int c) {
+    return c < L0C ? (int64_t)c * L0OPS : (int64_t)L0C * L0OPS + (int64_t)(c - L0C) * L1OPS;
+  }
+  __host__ __device__ static constexpr int chunk_ops(int c) { return c < L0C ? L0OPS : L1OPS; }
+};
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// two 16-row accumulator tiles of a group (+ bias) -> ReLU'd bf16 B fragment of the next layer
+__device__ __forceinline__ bf16x8 group_frag(const f32x4& t0, const f32x4& t1) {
+  const f32x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return relu_bf16(__builtin_convertvector(v, bf16x8));
+}
+__device__ __forceinline__ bf16x8 group_frag_bias(f32x4 t0, f32x4 t1, const float* bias, int base, int g) {
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + base + 4 * g);
+  const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + base + 16 + 4 * g);
+  return group_frag(t0 + b0, t1 + b1);
+}
+
+// Logits of sample tile s: output o of sample n sits in lane n + 16 (o >> 2), register o & 3.  Lanes
+// 16s .. 16s + 15 gather their sample's nine and emit it (32 samples per wave).
+__device__ __forceinline__ void emit_logits16(const f32x4 (&lg)[2], const float* b2, int64_t row0, int64_t rows,
+                                              int lane, const MlpArgs& a) {
+  const int n = lane & 15, part = lane >> 4;
+  f32x16 z16{};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float v[9];
+#pragma unroll
+    for (int o = 0; o < 9; ++o) v[o] = __shfl(lg[s][o & 3], n + 16 * (o >> 2));
+    if (part == s) {
+#pragma unroll
+      for (int o = 0; o < 9; ++o) z16[o] = v[o];
+    }
+  }
+  const int64_t row = row0 + 16 * part + n;
+  if (part < 2 && row < rows) {
+    constexpr int OUT = 9;
+    float z[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) z[o] = z16[o] + b2[o];
+    if (a.logits) {
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) a.logits[row * OUT + o] = z[o];
+    }
+    if (a.actions) {
+      float best = -INFINITY;
+      int arg = 0;
+      if (a.explore) {
+        uint32_t u32[12];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const uint4 v = philox10(make_uint4((uint32_t)row, (uint32_t)(row >> 32), a.step, (PUR_MLP << 24) | (uint32_t)b),
+                                   a.k0, a.k1);
+          u32[4 * b] = v.x;
+          u32[4 * b + 1] = v.y;
+          u32[4 * b + 2] = v.z;
+          u32[4 * b + 3] = v.w;
+        }
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          const float u = ((float)(u32[o] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+          const float v = z[o] - __logf(-__logf(u));
+          if (v > best) { best = v; arg = o; }
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < OUT; ++o)
+          if (z[o] > best) { best = z[o]; arg = o; }   // first maximum wins (numpy/torch argmax)
+      }
+      a.actions[row] = arg;
+    }
+  }
+}
+
+template <class N>
+__global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
+  // ONE __shared__ object (see k_mlp)
+  __shared__ __attribute__((aligned(16))) u32x4 lds[N::STAGES * N::SOPS * 64 + N::H1 / 4];
+  float* b1s = reinterpret_cast<float*>(lds + N::STAGES * N::SOPS * 64);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  const u32x4* chunks = static_cast<const u32x4*>(a.packed);
+  const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
+  const float* b2 = gb + N::H0 + N::H1;
+  const int64_t ntask = (a.rows + N::ROWS - 1) / N::ROWS;
+  const int my_tasks = (int)((ntask - blockIdx.x + gridDim.x - 1) / gridDim.x);
+
+  for (int i = tid; i < N::H1; i += N::MT) b1s[i] = gb[N::H0 + i];
+  auto stage_of = [&](int gg) { return lds + (gg & 1) * (N::SOPS * 64); };
+  auto fetch = [&](int gg) {
+    if (gg < my_tasks * N::NCH) {
+      const int c = gg % N::NCH;
+      stage_chunk<N>(chunks + N::chunk_off(c) * 64, stage_of(gg), N::chunk_ops(c), w, lane);
+    }
+  };
+  fetch(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+
+  // X^T fragments xb[q][s]: lane (n, g) holds features 32q + 8g + j of sample 16s + n of the wave
+  bf16x8 xb[N::KQ0][2];
+  const bool xf = a.xfrag != nullptr;
+  auto load_x = [&](int64_t task_i) {
+    const int64_t r0 = task_i * N::ROWS + w * 32;
+    if (xf) {
+      // wh_observe_x's 32x32x16 fragment order: 16-byte chunk ((tile * KQX + q16) * 64 + h * 32 + r)
+      // holds features 16 q16 + 8 h + j of row r of the 32-row tile
+      int64_t tile = task_i * N::WAVES + w;
+      tile = tile * 32 < a.rows ? tile : 0;
+      const u32x4* src = a.xfrag + tile * (N::KQX * 64);
+#pragma unroll
+      for (int q = 0; q < N::KQ0; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int q16 = 2 * q + (g >> 1);
+          xb[q][s] = q16 < N::KQX ? frag(src + q16 * 64 + (g & 1) * 32 + 16 * s + n) : bf16x8{};
+        }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int64_t row = r0 + 16 * s + n;
+        const bool lv = row < a.rows;
+        const float* x = a.obs + (lv ? row : 0) * N::IN;
+#pragma unroll
+        for (int q = 0; q < N::KQ0; ++q) {
+          f32x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 32 * q + 8 * g + j;
+            const float xv = x[k < N::IN ? k : N::IN - 1];
+            v[j] = k < N::IN ? (lv ? xv : 0.0f) : (k < N::IN + 2 ? 1.0f : 0.0f);
+          }
+          xb[q][s] = __builtin_convertvector(v, bf16x8);
+        }
+      }
+    }
+  };
+  if (my_tasks > 0) load_x(blockIdx.x);
+
+  for (int it = 0; it < my_tasks; ++it) {
+    const int64_t task = blockIdx.x + (int64_t)it * gridDim.x;
+    const int base = it * N::NCH;
+    const bool has_next = it + 1 < my_tasks;
+    f32x4 lg[2] = {f32x4{}, f32x4{}};
+    if constexpr (N::MODE == 0) {
+      bf16x8 hb[N::G0][2];
+#pragma unroll
+      for (int c = 0; c < N::L0C; ++c) {
+        const int gg = base + c;
+        fetch(gg + 1);
+        f32x4 acc[2][2];
+        stream_ops<N::L0OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
+          const int m = i / N::U0, k = i % N::U0, rt = k / N::KQ0, q = k % N::KQ0;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc[rt][s2]);
+          if (k == N::U0 - 1) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) hb[c * N::L0T + m][s2] = group_frag(acc[0][s2], acc[1][s2]);
+          }
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+      for (int d = 0; d < N::L1C; ++d) {
+        const int gg = base + N::L0C + d;
+        fetch(gg + 1);
+        // the next task's X during the last chunk (X is dead once layer 0 is done; loading it for
+        // the whole of layer 1 would keep its registers live beside all of layer 0's fragments)
+        if (d == N::L1C - 1 && has_next) load_x(task + gridDim.x);
+        f32x4 acc[2][2];
+        stream_ops<N::L1OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
+          const int uu = i / N::U1, k = i % N::U1;
+          if (k < 2 * N::G0) {
+            const int rt = k / N::G0, m = k % N::G0;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = mfma16(af, hb[m][s2], m == 0 ? f32x4{} : acc[rt][s2]);
+          } else {
+            const int u = d * N::L1T + uu;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              lg[s2] = mfma16(af, group_frag_bias(acc[0][s2], acc[1][s2], b1s, 32 * u, g), lg[s2]);
+          }
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+    } else {
+      f32x4 acc1[2 * N::G1][2];
+#pragma unroll
+      for (int v = 0; v < 2 * N::G1; ++v) acc1[v][0] = acc1[v][1] = f32x4{};
+      for (int c = 0; c < N::L0C; ++c) {
+        const int gg = base + c;
+        fetch(gg + 1);
+        f32x4 acc0[2][2];
+        bf16x8 hb0[2];
+        stream_ops<N::L0OPS, 4, 1>(stage_of(gg), lane, [&](int i, bf16x8 af) {
+          const int k = i % N::U0;
+          if (k < 2 * N::KQ0) {
+            const int rt = k / N::KQ0, q = k % N::KQ0;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) acc0[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc0[rt][s2]);
+            if (k == 2 * N::KQ0 - 1) {
+#pragma unroll
+              for (int s2 = 0; s2 < 2; ++s2) hb0[s2] = group_frag(acc0[0][s2], acc0[1][s2]);
+            }
+          } else {
+            const int v = k - 2 * N::KQ0;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) acc1[v][s2] = mfma16(af, hb0[s2], acc1[v][s2]);
+          }
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+      {
+        const int gg = base + N::L0C;
+        fetch(gg + 1);
+        if (has_next) load_x(task + gridDim.x);
+        stream_ops<N::L1OPS, 4, 1>(stage_of(gg), lane, [&](int u, bf16x8 af) {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            lg[s2] = mfma16(af, group_frag_bias(acc1[2 * u][s2], acc1[2 * u + 1][s2], b1s, 32 * u, g), lg[s2]);
+        });
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
+    }
+    emit_logits16(lg, b2, task * N::ROWS + w * 32, a.rows, lane, a);
+  }
+}
+
 // ------------------------------------------------------------------------------------- f32 mode
 // The same network in exact f32 (the reference policy is TF fp32): every layer on
 // v_mfma_f32_32x32x2_f32, whose result is bit-for-bit a k-ordered f32 fmaf chain, so logits differ
@@ -620,6 +890,63 @@ std::vector<uint8_t> pack(const float* w0, const float* b0, const float* w1, con
   return blob;
 }
 
+// Net16 blob: operands of 16 rows x 32 k, lane l = row l&15, k 8(l>>4)+j; layer-0 k order natural
+// (X^T from memory), layers 1-2 in kperm16 order (the accumulator-as-operand fragments).
+template <class N>
+std::vector<uint8_t> pack16(const float* w0, const float* b0, const float* w1, const float* b1,
+                            const float* w2, const float* b2) {
+  std::vector<uint8_t> blob(N::BYTES, 0);
+  uint16_t* f = reinterpret_cast<uint16_t*>(blob.data());
+  auto put = [&](int64_t op, int lane, int j, float v) { f[(op * 64 + lane) * 8 + j] = to_bf16(v); };
+  auto kperm16 = [](int m, int l, int j) { const int g = l >> 4; return 32 * m + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4); };
+  auto w0op = [&](int64_t op, int rt, int q) {          // W0 [H0][IN] row tile rt, k-step q (+ b0 hi/lo columns)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * q + 8 * (l >> 4) + j, o = 16 * rt + (l & 15);
+        const float bh = from_bf16(to_bf16(b0[o]));
+        const float v = k < N::IN ? w0[(int64_t)o * N::IN + k] : k == N::IN ? bh : k == N::IN + 1 ? b0[o] - bh : 0.0f;
+        put(op, l, j, v);
+      }
+  };
+  auto w1op = [&](int64_t op, int rt, int m) {          // W1 [H1][H0] row tile rt, k-step m (layer-0 group)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) put(op, l, j, w1[(int64_t)(16 * rt + (l & 15)) * N::H0 + kperm16(m, l, j)]);
+  };
+  auto w2op = [&](int64_t op, int u) {                  // W2 [9][H1], rows padded to 16, k-step u
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int o = l & 15;
+        put(op, l, j, o < N::OUT ? w2[(int64_t)o * N::H1 + kperm16(u, l, j)] : 0.0f);
+      }
+  };
+  for (int c = 0; c < N::L0C; ++c)
+    for (int mm = 0; mm < N::L0T; ++mm) {
+      const int t = c * N::L0T + mm;                     // layer-0 group
+      const int64_t base = N::chunk_off(c) + (int64_t)mm * N::U0;
+      for (int rt = 0; rt < 2; ++rt)
+        for (int q = 0; q < N::KQ0; ++q) w0op(base + rt * N::KQ0 + q, 2 * t + rt, q);
+      if (N::MODE == 1)
+        for (int v = 0; v < 2 * N::G1; ++v) w1op(base + 2 * N::KQ0 + v, v, t);
+    }
+  if (N::MODE == 0) {
+    for (int d = 0; d < N::L1C; ++d)
+      for (int uu = 0; uu < N::L1T; ++uu) {
+        const int u = d * N::L1T + uu;                   // layer-1 group
+        const int64_t base = N::chunk_off(N::L0C + d) + (int64_t)uu * N::U1;
+        for (int rt = 0; rt < 2; ++rt)
+          for (int m = 0; m < N::G0; ++m) w1op(base + rt * N::G0 + m, 2 * u + rt, m);
+        w2op(base + 2 * N::G0, u);
+      }
+  } else {
+    for (int u = 0; u < N::G1; ++u) w2op(N::chunk_off(N::L0C) + u, u);
+  }
+  float* bias = reinterpret_cast<float*>(blob.data() + N::BIAS_OFF);
+  memcpy(bias, b0, 4 * N::H0);
+  memcpy(bias + N::H0, b1, 4 * N::H1);
+  memcpy(bias + N::H0 + N::H1, b2, 4 * N::OUT);
+  return blob;
+}
+
 template <class N>
 std::vector<uint8_t> pack_f32(const float* w0, const float* b0, const float* w1, const float* b1,
                               const float* w2, const float* b2) {
@@ -669,6 +996,12 @@ MlpKernel make_mlp() {
   return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp<N>, pack<N>};
 }
 
+template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T>
+MlpKernel make_mlp16() {
+  using N = Net16<IN, H0, H1, WAVES, MODE, L0T, L1T>;
+  return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp16<N>, pack16<N>};
+}
+
 template <int IN, int H0, int H1, int PASSES>
 MlpKernel make_mlp_f32() {
   using N = NetF<IN, H0, H1, PASSES>;
@@ -676,7 +1009,18 @@ MlpKernel make_mlp_f32() {
 }
 
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
-  // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml
+  // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml:
+  // bf16 on 16x16x32 tiles (k_mlp16); WH_MLP_LEGACY=1 selects the 32x32x16 kernel (A/B runs; a
+  // blob is packed for the kernel of its process)
+  static const bool legacy = getenv("WH_MLP_LEGACY") != nullptr;
+  static const MlpKernel reg16[] = {
+      make_mlp16<37, 256, 256, 8, 0, 8, 4>(),      // Small
+      make_mlp16<82, 512, 512, 8, 0, 8, 2>(),      // Medium
+      make_mlp16<145, 1024, 256, 8, 1, 2, 1>(),    // Large
+  };
+  if (d && d->out_dim == 9 && d->precision == WH_MLP_BF16 && !legacy)
+    for (const auto& k : reg16)
+      if (k.in == d->in_dim && k.h0 == d->hidden0 && k.h1 == d->hidden1) return &k;
   static const MlpKernel reg[] = {
       // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk,
       // next-task X prefetch): 8 waves = two per SIMD (256 registers each)
