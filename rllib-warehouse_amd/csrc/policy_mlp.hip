@@ -1010,11 +1010,12 @@ MlpKernel make_mlp_f32() {
 
 const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // the policy_model shapes of scripts/experiments/warehouse-{small,medium,large}-sac/*.yaml:
-  // bf16 on 16x16x32 tiles (k_mlp16); WH_MLP_LEGACY=1 selects the 32x32x16 kernel (A/B runs; a
-  // blob is packed for the kernel of its process)
+  // bf16 on 16x16x32 tiles (k_mlp16) for Medium and Large, +4-7 % over the 32x32x16 kernel on the
+  // same box; Small keeps the 32x32x16 kernel, whose next-task X prefetch fits its registers there
+  // (16x16x32 without it: -3 to -8 %, profiles/r04_mlp16_ab.txt).  WH_MLP_LEGACY=1 selects the
+  // 32x32x16 kernel everywhere (A/B runs; a blob is packed for the kernel of its process).
   static const bool legacy = getenv("WH_MLP_LEGACY") != nullptr;
   static const MlpKernel reg16[] = {
-      make_mlp16<37, 256, 256, 8, 0, 8, 4>(),      // Small
       make_mlp16<82, 512, 512, 8, 0, 8, 2>(),      // Medium
       make_mlp16<145, 1024, 256, 8, 1, 2, 1>(),    // Large
   };
