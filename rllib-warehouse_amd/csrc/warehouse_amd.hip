@@ -1506,8 +1506,30 @@ struct FastRun {
   uint8_t* drow;
   int64_t rstride;
   LazyGrid lg;
+  uint32_t act[POLICY == POL_EXTERNAL ? C::NAM : 1];   // external actions of the (single) step
   __device__ __forceinline__ FastRun(const StepParams& a, int64_t e)
       : rrow(a.rewards + e * C::NAM), drow(a.dones + e), rstride(a.B * C::NAM), lg{true, 0u} {}   // the grid starts empty (k_step)
+  // POL_EXTERNAL: the step's actions, loaded with the state in the prologue (their HBM latency then
+  // overlaps the table loads instead of sitting on the first step)
+  __device__ __forceinline__ void load_actions(const StepParams& a, int64_t e) {
+    if constexpr (POLICY == POL_EXTERNAL) {
+      if constexpr (C::NAM % 4 == 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.actions + e * C::NAM);
+#pragma unroll
+        for (int q = 0; q < C::NAM / 4; ++q) {
+          const uint4 v = src[q];
+          act[4 * q] = v.x; act[4 * q + 1] = v.y; act[4 * q + 2] = v.z; act[4 * q + 3] = v.w;
+        }
+      } else {
+        const uint2* src = reinterpret_cast<const uint2*>(a.actions + e * C::NAM);
+#pragma unroll
+        for (int q = 0; q < C::NAM / 2; ++q) {
+          const uint2 v = src[q];
+          act[2 * q] = v.x; act[2 * q + 1] = v.y;
+        }
+      }
+    }
+  }
 
   __device__ __forceinline__ void step(const StepParams& a, Regs<C>& s, Lds<C>& L, Slots<C>* RS, const Keys& k,
                                        uint32_t gid, int64_t e, int tid, int stp) {
@@ -1517,7 +1539,10 @@ struct FastRun {
     constexpr int ablate = 0;
 #endif
     uint32_t d[C::NAM];
-    if (ablate & 1) {
+    if constexpr (POLICY == POL_EXTERNAL) {
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) d[i] = L.mv(act[i] > 8u ? 4u : act[i]);   // MOVES[a]; others stay
+    } else if (ablate & 1) {
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
     } else {
@@ -1581,7 +1606,13 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
   LazyGrid lg{true, 0u};   // the grid starts empty (k_step)
   for (int stp = 0; stp < a.steps; ++stp) {
     uint32_t d[C::NAM];
-    if (ablate & 1) {
+    if constexpr (POLICY == POL_EXTERNAL) {   // (wh_vector_step's fast case: one step)
+#pragma unroll
+      for (int i = 0; i < C::NAM; ++i) {
+        const uint32_t mv = (uint32_t)a.actions[e * C::NAM + i];
+        d[i] = L.mv(mv > 8u ? 4u : mv);
+      }
+    } else if (ablate & 1) {
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) d[i] = L.mv((uint32_t)((i + stp) % 9));
     } else {
@@ -1949,21 +1980,21 @@ template <int R, int NAM>
 __constant__ ObsSrc<R, NAM> kObsSrcF =
     make_obs_src<R, NAM, FImg<R>::A0, FImg<R>::G0, FImg<R>::P0, FImg<R>::Q0>();
 
-template <class C>
+template <class C, int NBUF = 1>
 struct SampLds {
   static constexpr int IMG = FImg<C::R>::IMG, SRCW = ObsSrc<C::R, C::NAM>::W;
-  // two image buffers: step k's images are written while step k-1's rows stream from the other
-  alignas(16) uint8_t img[2][BT][IMG];
-  uint32_t lim[2][BT];     // n * L (floats of live rows) | fresh << 31
+  // multi-step launches: two image buffers, step k's images written while step k-1's rows stream
+  // from the other
+  alignas(16) uint8_t img[NBUF][BT][IMG];
+  uint32_t lim[NBUF][BT];  // n * L (floats of live rows) | fresh << 31
   uint32_t src[2][SRCW];
-  uint32_t next[2];        // row chunks handed out (write_rows), per image buffer
 };
 
 // core.py:224-260 / 371-432 for the env of this lane, from its registers after the step: the image
 // k_observe builds from the packed state (n, availability, delivery targets, positions, the open
 // requests in ascending pickup order with their pickup and delivery cells).
-template <class C>
-__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C>& O, int tid, int na,
+template <class C, int NBUF>
+__device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, SampLds<C, NBUF>& O, int tid, int na,
                                             int buf) {
   using F = FImg<C::R>;
   uint8_t* im = O.img[buf][tid];
@@ -2007,48 +2038,29 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
 }
 
 // Rows of the workgroup's envs from image buffer `buf`: one contiguous [nenv x na x L] f32 region at
-// `rows` (its first env's first float), float4 per lane (na * L % 4 == 0 and 16-byte alignment:
-// checked on the host).  The region is handed out in chunks of kRowChunk float4s from a counter in
-// LDS (O.next[buf], zero on entry), one chunk per wave at a time, so waves that join late (the step
-// lanes, after their step) take what is left instead of a fixed share.
-constexpr uint32_t kRowChunk = 1024;
-template <class C>
-__device__ __forceinline__ void write_rows(SampLds<C>& O, int buf, float* __restrict__ rows, uint32_t nenv,
-                                           uint32_t qe, int tid) {
+// `rows` (its first env's first float), float4 per lane over all 2 x BT lanes, q = tid + 2 BT i (na * L
+// % 4 == 0 and 16-byte alignment: checked on the host).  (Chunks handed out from an LDS counter, so
+// that the step lanes of a multi-step launch take less once they join late, measured 1.5 us slower
+// on a 1-step launch and no faster on 20- and 100-step ones: profiles/r04_rows_ab.txt.)
+template <class C, int NBUF>
+__device__ __forceinline__ void write_rows(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
+                                           uint32_t nenv, uint32_t qe, int tid) {
   const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
   const uint32_t total = nenv * qe;
-  const uint32_t lane = (uint32_t)tid & 63u;
   f32x4* out4 = reinterpret_cast<f32x4*>(rows);
-#ifdef WH_ROWS_STATIC   // (A/B builds: a fixed share per lane, q = tid + 2 BT i)
-  for (uint32_t q0 = (uint32_t)tid - lane; q0 < total; q0 += 2 * BT) {
-    {
-      const uint32_t q = q0 + lane;
-      if (q < total) {
-#else
-  for (;;) {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&O.next[buf], 1u);
-    const uint32_t q0 = (uint32_t)__builtin_amdgcn_readfirstlane(c) * kRowChunk;
-    if (q0 >= total) break;
-#pragma unroll 4
-    for (uint32_t u = 0; u < kRowChunk; u += 64) {
-      const uint32_t q = q0 + u + lane;
-      if (q < total) {
-#endif
-        const uint32_t el4 = __umulhi(q, magic);
-        const uint32_t k4 = q - el4 * qe;
-        const uint32_t lim = O.lim[buf][el4];
-        const uint32_t sw = O.src[lim >> 31][k4];
-        const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
-        const uint8_t* im = O.img[buf][el4];
-        f32x4 v;
-        v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
-        v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
-        v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
-        v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
-        out4[q] = v;
-      }
-    }
+  for (uint32_t q = tid; q < total; q += 2 * BT) {
+    const uint32_t el4 = __umulhi(q, magic);
+    const uint32_t k4 = q - el4 * qe;
+    const uint32_t lim = O.lim[buf][el4];
+    const uint32_t sw = O.src[lim >> 31][k4];
+    const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
+    const uint8_t* im = O.img[buf][el4];
+    f32x4 v;
+    v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
+    v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
+    v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
+    v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
+    out4[q] = v;
   }
 }
 
@@ -2063,11 +2075,11 @@ __device__ __forceinline__ void write_rows(SampLds<C>& O, int buf, float* __rest
 // action-dict order (ORDERED), an optional env mask -- envs not stepped keep their state and still
 // get their rows -- and the launch options of k_step's generic instance (episode metrics, odd agent
 // counts).
-template <class C, int POLICY, bool ORDERED, bool FAST>
+template <class C, int POLICY, bool ORDERED, bool FAST, bool MULTI = false>
 __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restrict__ obs) {
   __shared__ Lds<C> L;
-  __shared__ SampLds<C> O;
-  __shared__ std::conditional_t<FAST, Slots<C>, NoSlots> RS;   // reset slots: multi-step launches
+  __shared__ SampLds<C, MULTI ? 2 : 1> O;
+  __shared__ std::conditional_t<MULTI, Slots<C>, NoSlots> RS;   // reset slots: multi-step launches
   const int tid = threadIdx.x;
   const bool stepper = tid < BT;
   const int64_t e0 = (int64_t)blockIdx.x * BT;
@@ -2076,13 +2088,16 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   const bool stepped = loaded && (FAST || !a.mask || a.mask[e]);       // and it is stepped
   const int na = FAST ? C::NAM : a.na;
   RawEnv<C> raw;
-  if (loaded) load_env_issue<C>(raw, a.state, a.B, e, na);
+  FastRun<C, POLICY, MULTI> run(a, e);
+  if (loaded) {
+    load_env_issue<C>(raw, a.state, a.B, e, na);
+    if constexpr (FAST) run.load_actions(a, e);
+  }
   if (stepper) {
     load_tables<C>(L.tbl, a.tables);
   } else {
     const uint32_t* srcg = &kObsSrcF<C::R, C::NAM>.w[0][0];
     for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
-    if (tid - BT < 2) O.next[tid - BT] = 0u;
   }
   __syncthreads();
   const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
@@ -2098,14 +2113,10 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;
     }
   }
-  if constexpr (FAST) {
+  if constexpr (FAST && MULTI) {
     if (loaded) RS.rs_ep[tid] = s.epi;   // reset slots start stale (!= epi + 1)
-    FastRun<C, POLICY, true> run(a, e);
     const int64_t step_floats = a.B * (int64_t)(C::NAM * C::L);
     for (int it = 0; it <= a.steps; ++it) {   // (every wave reaches every barrier)
-      // iteration it streams buffer (it-1)%2 with counter next[(it-1)%2]; the counter iteration
-      // it+1 uses was last used in iteration it-1, whose readers all passed the barrier before this
-      if (tid == BT && it > 0) O.next[it & 1] = 0u;
       if (loaded && it < a.steps) {
         run.step(a, s, L, &RS, k, gid, e, tid, it);
         write_image<C>(s, L, O, tid, C::NAM, it & 1);
@@ -2114,6 +2125,14 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       __syncthreads();
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e, na, tid);
+  } else if constexpr (FAST) {   // one step
+    if (loaded) {
+      run.step(a, s, L, nullptr, k, gid, e, tid, 0);
+      store_env<C>(s, L, a.state, a.B, e, na, tid);
+      write_image<C>(s, L, O, tid, C::NAM, 0);
+    }
+    __syncthreads();
+    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
     if (stepped) {
       run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
@@ -2347,6 +2366,7 @@ struct Kernels {
   void (*step_fast[3])(StepParams);   // [policy]: greedy / random fused rollouts (NAM even), else null
   void (*step_ordered)(StepParams);
   void (*sampler[3])(StepParams, float*);   // [policy]: fused step + rows (k_sampler), NAM even, else null
+  void (*sampler_multi[3])(StepParams, float*);   // [policy]: the same, K steps per launch (greedy / random)
   void (*vsampler[2])(StepParams, float*);  // [ordered]: wh_vector_step's step + rows (external actions)
   void (*reset)(ResetParams);
   void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // 8 / 16 / 64 envs per WG
@@ -2361,16 +2381,21 @@ Kernels make_kernels() {
   k.step[0] = k_step<C, POL_EXTERNAL, false, false>;
   k.step[1] = k_step<C, POL_GREEDY, false, false>;
   k.step[2] = k_step<C, POL_RANDOM, false, false>;
-  k.step_fast[0] = nullptr;
+  k.step_fast[0] = nullptr;   // (set below for even agent counts: wh_vector_step's common case)
   k.sampler[0] = k.sampler[1] = k.sampler[2] = nullptr;
+  k.sampler_multi[0] = k.sampler_multi[1] = k.sampler_multi[2] = nullptr;
   // the multi-step sampler holds the step's LDS, its reset slots and two image buffers
-  constexpr bool sampler_fits = sizeof(Lds<C>) + sizeof(Slots<C>) + sizeof(SampLds<C>) <= 160 * 1024;
+  constexpr bool sampler_fits = sizeof(Lds<C>) + sizeof(Slots<C>) + sizeof(SampLds<C, 2>) <= 160 * 1024;
   if constexpr (NAM % 2 == 0) {
+    k.step_fast[0] = k_step<C, POL_EXTERNAL, false, true>;
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
+    k.sampler[0] = k_sampler<C, POL_EXTERNAL, false, true>;
+    k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
+    k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
     if constexpr (sampler_fits) {
-      k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
-      k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
+      k.sampler_multi[1] = k_sampler<C, POL_GREEDY, false, true, true>;
+      k.sampler_multi[2] = k_sampler<C, POL_RANDOM, false, true, true>;
     }
   } else {
     k.step_fast[1] = k.step_fast[2] = nullptr;
@@ -2793,7 +2818,9 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
   const Kernels* k = nullptr;
   const uint32_t* tab = nullptr;
   if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK) {
-    void (*fk)(StepParams, float*) = k->vsampler[order ? 1 : 0];
+    // the fast instance when the step resolved to it (every env stepped in ascending order, no
+    // metrics, auto-reset: RLlib's common case), else the generic one
+    void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
     if (fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
       hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
       return hip_err(hipGetLastError());
@@ -2867,9 +2894,10 @@ int wh_sampler_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t
   const uint32_t* tab = nullptr;
   if ((rc = prepare(cfg, B, stream, &g, &k, &tab)) != WH_OK) return rc;
   static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
-  if (!unfused && l.kern == k->step_fast[policy] && k->sampler[policy] && fused_ok(k->sampler[policy]) &&
-      (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
-    hipLaunchKernelGGL(k->sampler[policy], grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
+  void (*fk)(StepParams, float*) = steps == 1 ? k->sampler[policy] : k->sampler_multi[policy];
+  if (!unfused && l.kern == k->step_fast[policy] && fk && fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 &&
+      (uintptr_t)obs % 16 == 0) {
+    hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
     return hip_err(hipGetLastError());
   }
   // otherwise: the same steps one launch (pair) at a time

@@ -584,7 +584,9 @@ def test_fused_vector_step_equals_two_launch_route(wh, variant, na, train, B, ma
     actions, optional env mask and action-dict order, episode metrics) where its step code keeps its
     registers; it must equal the two launches it replaces -- the step alone (observe=False) then
     wh_observe -- in rewards, dones (stepped envs), rows of EVERY env (masked-out envs keep theirs),
-    episode metrics and state, over 210 steps with auto-reset."""
+    episode metrics and state, over 210 steps with auto-reset.  Without mask, order and metrics the
+    fused launch runs the fast (fused-rollout) step instance with external actions; the comparison
+    then steps b with an all-true mask, i.e. through the generic instance."""
     import torch
 
     seed, K = 23, 210
@@ -605,7 +607,10 @@ def test_fused_vector_step_equals_two_launch_route(wh, variant, na, train, B, ma
             drop = rng.random((B, NA)) < 0.2
             order = torch.from_numpy(np.where(np.cumsum(drop, axis=1) > 0, -1, perm).astype(np.int32))
         oa, ra, da = a.vector_step(acts, autoreset=True, mask=mask, order=order)
-        _, rb, db = b.vector_step(acts, autoreset=True, mask=mask, order=order, observe=False)
+        # b: the two launches, and with an all-true mask where a has none, so that b's step is the
+        # generic instance while a's (no mask, no order, no metrics) is the fast one
+        mb = torch.ones(B, dtype=torch.bool) if mask is None else mask
+        _, rb, db = b.vector_step(acts, autoreset=True, mask=mb, order=order, observe=False)
         ob_ = b.observe()
         live = slice(None) if mask is None else mask.to(ra.device)
         assert torch.equal(ra[live], rb[live]) and torch.equal(da[live], db[live]), f"step {s}"
