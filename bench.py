@@ -688,6 +688,9 @@ def main():
             "ms_per_step": el3 * 1e3 / Ks,
             "kernel_split_ms": split,
             "two_launch_form_ms": split["two-launch form: k_step (1-step rollout)"] + split["two-launch form: k_observe"],
+            # what the step adds to a launch that writes the same rows: the fused launch minus the
+            # row-writing kernel alone (k_observe: same rows, same state read, no step)
+            "step_share_ms": fms - split["two-launch form: k_observe"],
             "two_stream_pipeline": {
                 "workload": "the two-launch form as SamplerPipeline: the rows of step s on a side stream while "
                             "step s+1 runs (state double-buffered); slower -- the step launch's workgroups only "

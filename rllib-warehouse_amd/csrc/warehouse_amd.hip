@@ -36,6 +36,7 @@
 namespace {
 
 constexpr int BT = 256;  // lanes (= envs) per workgroup
+constexpr uint32_t ROWB = 2 * BT;   // bytes per pickup-point row of the LDS pickup plane
 
 enum Policy { POL_EXTERNAL = 0, POL_GREEDY = 1, POL_RANDOM = 2 };
 enum Purpose : uint32_t { PUR_RESET = 1, PUR_REGEN = 2, PUR_POLICY = 3, PUR_RANDOM = 4 };
@@ -71,9 +72,6 @@ constexpr int kUKeyMinNam = WH_UKEY_MIN_NAM;
 #define WH_BIAS_MAX_NAM 64
 #endif
 constexpr int kRevSplitMaxNam = WH_REV_SPLIT_MAX_NAM, kBiasMaxNam = WH_BIAS_MAX_NAM;
-#ifndef WH_PK32   // (A/B builds: -DWH_PK32=0 keeps 16-bit pickup cells everywhere)
-#define WH_PK32 1
-#endif
 #ifndef WH_NO_REGEN_HOIST
 constexpr bool kRegenHoist = true;
 #else
@@ -84,19 +82,12 @@ constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle ag
 constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 
 // Shared (per-workgroup) table layout in bytes; built identically by build_tables() on the host.
-// The (pickup cell, tag) pairs and the delivery cells are also stored as 32 copies, entry-major with
-// one copy per LDS bank (rp32: [P+1][32] x 8 B, dst32: [DP][32] x 4 B): lane l reads copy l % 32,
-// whose bank is its own whatever entry it asks for, so the data-dependent reads of the policy's
-// request walk and of the pickup's delivery lookup are conflict-free (one copy: random entries over
-// 32 banks, ~3-way conflicts on every such read -- SQ_LDS_BANK_CONFLICT, profiles/pmc_traffic.json).
 struct TableLayout {
-  int cell, rp, tag, dst, mv, valid, rp32, dst32, bytes;
+  int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
       : cell(0), rp(256 * D), tag(256 * D + 4), dst(256 * D + 8 * (P + 1)),   // rp/tag interleaved
         mv(256 * D + 8 * (P + 1) + 4 * DP), valid(256 * D + 8 * (P + 1) + 4 * DP + 48),
-        rp32((256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV + 7) & ~7),
-        dst32(((256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV + 7) & ~7) + 256 * (P + 1)),
-        bytes(((256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV + 7) & ~7) + 256 * (P + 1) + 128 * DP) {}
+        bytes(256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
 
 template <int D_, int R_, int NR_, int NAM_>
@@ -110,12 +101,6 @@ struct Cfg {
   static constexpr int TBLW = T.bytes / 4;
   static constexpr int TBL4 = (TBLW + 3) / 4;           // 16-byte chunks (device copy padded to them)
   static constexpr int L = 9 * R + 1;                    // observation row length
-  // pickup plane cells of 32 bits (a lane's cell in its own bank: conflict-free whatever points the
-  // lanes of a wave touch) when the step kernel's LDS allows, else 16 bits (2 lanes per bank word)
-  static constexpr int LDS32 = 16 * TBL4 + 4 * D * 256 + 4 * (P + 1) * 256 + 4 * NAM * 256 +
-                               (4 * NAM + 2 * R + 16) * 256;
-  static constexpr bool PK32 = WH_PK32 && LDS32 <= 150 * 1024;
-  static constexpr uint32_t ROWB = (PK32 ? 4 : 2) * 256;   // bytes per pickup-point row
   static_assert(D <= 32, "positions are 5-bit fields (occupancy rows are 32-bit words)");
   static_assert(P <= 64 && DP <= 64, "bitmask sets hold at most 64 points");
   static_assert(NAM <= R, "agents <= requests (core.py:89)");
@@ -285,7 +270,7 @@ struct Lds {
   // (low 8 bits).  Row P is scratch: predicated stores of lanes with nothing to write go there.
   // One 16-bit cell per (point, lane) makes every per-point access a single ds op whose address
   // is j * BT + tid, and keeps the pickup table out of the VGPRs.
-  std::conditional_t<C::PK32, uint32_t, uint16_t> pkp[C::P + 1][BT];
+  uint16_t pkp[C::P + 1][BT];
   // Agent words when processing in action-dict order; afterwards the reward-row staging area.
   // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
   alignas(16) uint32_t agl[C::NAM][BT];
@@ -296,8 +281,8 @@ struct Lds {
   }
 
   // (pickup cell, greedy tag) of point j: one 8-byte LDS read
-  __device__ __forceinline__ uint2 rtag(uint32_t j) const {   // (bank copy of this lane)
-    return reinterpret_cast<const uint2*>(&tbl[C::T.rp32 / 4])[j * 32u + (__lane_id() & 31u)];
+  __device__ __forceinline__ uint2 rtag(uint32_t j) const {
+    return reinterpret_cast<const uint2*>(&tbl[C::T.rp / 4])[j];
   }
   __device__ __forceinline__ uint32_t mv(uint32_t a) const { return tbl[C::T.mv / 4 + a]; }
   __device__ __forceinline__ uint32_t valid_cell(uint32_t v) const { return tbl[C::T.valid / 4 + v]; }
@@ -313,17 +298,15 @@ struct Lds {
     return (uint32_t)(reinterpret_cast<const char*>(&pkp[0][0]) - reinterpret_cast<const char*>(this));
   }
   __device__ __forceinline__ const uint8_t* row_byte(uint32_t cv, int tid) const {
-    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - C::ROWB) + cv * C::ROWB + (C::ROWB / BT) * tid;
+    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
   }
   __device__ __forceinline__ uint8_t* row_byte(uint32_t cv, int tid) {
-    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - C::ROWB) + cv * C::ROWB + (C::ROWB / BT) * tid;
+    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
   }
   // Delivery cell of a target byte (target + 1; 0 reads the word before the table: never used) in
   // agent-word form: x << 8 | y << 24 in the target bytes, ones in the position bytes, so a pickup
   // is one AND of the (idle: 0xFF target bytes) agent word.
-  __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const {   // (bank copy of this lane)
-    return tbl[C::T.dst32 / 4 - 32 + tb * 32u + (__lane_id() & 31u)];
-  }
+  __device__ __forceinline__ uint32_t dst_tb(uint32_t tb) const { return tbl[C::T.dst / 4 - 1 + tb]; }
 };
 
 // Reset slots (fused rollout only: their own __shared__ object in that k_step instance, so the
@@ -2331,14 +2314,6 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   words.insert(words.end(), dst.begin(), dst.end());
   words.insert(words.end(), mv.begin(), mv.end());
   words.insert(words.end(), valid.begin(), valid.end());
-  while (words.size() % 2) words.push_back(0u);             // rp32: 8-byte aligned
-  for (int j = 0; j <= g.P; ++j)
-    for (int c = 0; c < 32; ++c) {
-      words.push_back(rp[j]);
-      words.push_back(tag[j]);
-    }
-  for (int d = 0; d < g.DP; ++d)
-    for (int c = 0; c < 32; ++c) words.push_back(dst[d]);
   return words;
 }
 
@@ -2411,16 +2386,13 @@ Kernels make_kernels() {
   k.sampler_multi[0] = k.sampler_multi[1] = k.sampler_multi[2] = nullptr;
   // the multi-step sampler holds the step's LDS, its reset slots and two image buffers
   constexpr bool sampler_fits = sizeof(Lds<C>) + sizeof(Slots<C>) + sizeof(SampLds<C, 2>) <= 160 * 1024;
-  constexpr bool sampler1_fits = sizeof(Lds<C>) + sizeof(SampLds<C, 1>) <= 160 * 1024;
   if constexpr (NAM % 2 == 0) {
     k.step_fast[0] = k_step<C, POL_EXTERNAL, false, true>;
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
-    if constexpr (sampler1_fits) {
-      k.sampler[0] = k_sampler<C, POL_EXTERNAL, false, true>;
-      k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
-      k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
-    }
+    k.sampler[0] = k_sampler<C, POL_EXTERNAL, false, true>;
+    k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
+    k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
     if constexpr (sampler_fits) {
       k.sampler_multi[1] = k_sampler<C, POL_GREEDY, false, true, true>;
       k.sampler_multi[2] = k_sampler<C, POL_RANDOM, false, true, true>;
@@ -2429,11 +2401,8 @@ Kernels make_kernels() {
     k.step_fast[1] = k.step_fast[2] = nullptr;
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
-  k.vsampler[0] = k.vsampler[1] = nullptr;
-  if constexpr (sampler1_fits) {
-    k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
-    k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
-  }
+  k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
+  k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
   k.observe[0] = k_observe<C, 8>;
   k.observe[1] = k_observe<C, 16>;
@@ -2852,7 +2821,7 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
     // the fast instance when the step resolved to it (every env stepped in ascending order, no
     // metrics, auto-reset: RLlib's common case), else the generic one
     void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
-    if (fk && fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+    if (fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
       hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
       return hip_err(hipGetLastError());
     }
