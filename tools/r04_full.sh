@@ -8,8 +8,10 @@ tail -1 gpurun_out/r04_smoke.log
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err || { tail -20 gpurun_out/r04_bench.err; exit 1; }
 python -c "
 import json; d=json.loads(open('gpurun_out/r04_bench.json').read().strip().splitlines()[-1])
-print('value', d['value'], 'kernel_ms', d['roofline']['kernel_ms'], 'frac', d['roofline']['frac'], 'bound', d['roofline']['bound'])
-print('sampler', d['sampler_path']['value'], d['sampler_path']['kernel_split_ms'])
+r=d['roofline']
+print('value', d['value'], 'kernel_ms', r['kernel_ms'], 'frac', r['frac'], 'bound', r['bound'], 'valu', (r.get('valu') or {}).get('frac'))
+print('sampler', d['sampler_path']['value'], d['sampler_path']['kernel_split_ms'], 'step share', d['sampler_path'].get('step_share_ms'))
+print('fragments', (d.get('sampler_fragments') or {}).get('value'), 'vector', (d.get('vector_path') or {}).get('value'))
 print('policy', d['policy_path']['value'], d['policy_path']['roofline']['frac'])
 print('desync', d['desync_episodes']['kernel_time_vs_synchronised'])
 print('cpu', d['cpu_baseline']['value'], d['cpu_baseline']['cores'])
