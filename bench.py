@@ -617,6 +617,9 @@ def main():
     import torch.distributed as dist
 
     world, rank, local = rank_info()
+    # one GPU per rank on the driver's node; a node with fewer devices than ranks (a rehearsal of the
+    # N > 1 path on one card) shares them round-robin (device_count() initialises nothing here)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)             # before any other GPU call of this rank
     if world > 1:
         dist.init_process_group("gloo")
