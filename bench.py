@@ -1,7 +1,12 @@
 """Benchmark: aggregate agent-steps/s of the device-resident greedy rollout (BASELINE.json config 3).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]      (N > 1: starts the N ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Without a launcher, --gpus N > 1 makes this process start N child processes with
+torch.distributed.run's environment (launch_ranks; the parent touches no GPU); under a launcher,
+WORLD_SIZE must equal --gpus.  More ranks than cards is refused unless --rehearse-shared-devices
+(then the line's metric says REHEARSAL and `devices` records the sharing).
 
 Workload (per GPU, weak scaling): WarehouseMedium, 8 agents, B = 65,536 envs, greedy policy
 (baseline/solvers.py:27-58) fused with Warehouse.step() (warehouse/core.py:262-442) and
@@ -186,6 +191,95 @@ def rank_info(environ=None):
     """(world, rank, local_rank) from the torch.distributed.run environment (1, 0, 0 without it)."""
     env = os.environ if environ is None else environ
     return int(env.get("WORLD_SIZE", "1")), int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+
+
+def check_world(gpus, environ=None):
+    """--gpus N against the launcher's environment.  Returns "launch" when this process must start the
+    N ranks itself (no WORLD_SIZE and N > 1), "run" otherwise; a WORLD_SIZE that differs from --gpus
+    is an error (the line would report a world size the command did not ask for)."""
+    env = os.environ if environ is None else environ
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher's WORLD_SIZE is {ws}; they must agree")
+    return "run"
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus, argv, environ=None, port=None):
+    """`python bench.py --gpus N` without a launcher: start N child processes of this script, one per
+    GPU, with torch.distributed.run's variables (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+    MASTER_PORT), wait for all of them and return the worst exit code.  The parent has imported
+    neither torch nor the library when it gets here: nothing in this process touches a GPU, and the
+    children are started as new processes (no exec).  Rank 0 prints the single JSON line.  If one
+    rank fails, the others (blocked in a barrier) are terminated by PID."""
+    import subprocess
+
+    base = dict(os.environ if environ is None else environ)
+    port = port or _free_port()
+    procs = []
+    for r in range(gpus):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WH_BENCH_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [None] * gpus
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
+
+
+def assign_device(local, world, device_count, shared_ok):
+    """The GPU of a rank: LOCAL_RANK, one per card.  A node with fewer cards than ranks is an error
+    unless the run is an explicit rehearsal (--rehearse-shared-devices), where ranks share cards
+    round-robin and the line says so (physical_devices, devices_shared).  Returns (index, shared)."""
+    if device_count < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if local < device_count:
+        return local, world > device_count
+    if not shared_ok:
+        raise SystemExit(f"bench.py: rank {local} needs a GPU of its own but the node has {device_count}; "
+                         "pass --rehearse-shared-devices for a rehearsal on shared cards (not a scaling measurement)")
+    return local % device_count, True
+
+
+# Environment switches the library reads that change which kernels run (A/B experiments).  A bench
+# line measured with one set does not describe the production path: refused unless --allow-overrides,
+# and recorded in the line either way.
+KERNEL_OVERRIDES = ("WH_SAMPLER_UNFUSED", "WH_MLP_LEGACY", "WH_MLP_ABLATE", "WH_ABLATE", "WAREHOUSE_AMD_LIB",
+                    "WAREHOUSE_AMD_AB")
+
+
+def kernel_overrides(environ=None):
+    env = os.environ if environ is None else environ
+    return {k: env[k] for k in KERNEL_OVERRIDES if k in env}
 
 
 def shard_offset(rank, envs_per_gpu):
@@ -589,6 +683,37 @@ def report(out, args):
     return out
 
 
+def plumbing_only(args, world, rank, dist):
+    """--plumbing-only: the multi-rank path end to end without a GPU (CPU tests of the self-launch):
+    gloo group, shard offsets, the barrier/max timing window around a host-side sleep, the aggregate
+    and rank 0's line with the host-core baseline.  No kernel runs; the line says so."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    B, NA, K = args.envs, args.agents, args.steps
+    elapsed = timed_window(lambda: time.sleep(0.05 * (rank + 1)), lambda: None, world, dist)
+    if world > 1:
+        import torch
+
+        offs = torch.tensor([shard_offset(rank, B)], dtype=torch.int64)
+        gathered = [torch.zeros_like(offs) for _ in range(world)]
+        dist.all_gather(gathered, offs)
+        offsets = [int(g.item()) for g in gathered]
+    else:
+        offsets = [0]
+    if rank == 0:
+        report({"metric": f"PLUMBING SELF-TEST, NOT A MEASUREMENT ({METRIC})",
+                "value": aggregate_rate(world, B, NA, K, elapsed), "unit": "agent-steps/s", "n_gpus": world,
+                "steps": K, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / K, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none: no kernel ran",
+                "config": {"workload": "plumbing self-test", "envs_per_gpu": B, "agents": NA,
+                           "shard_offsets": offsets,
+                           "launch": "self-launched ranks" if os.environ.get("WH_BENCH_SELF_LAUNCHED") else
+                                     ("launcher" if world > 1 else "single process")}}, args)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -611,15 +736,32 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = one per host core (host_cores())")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearse-shared-devices", action="store_true",
+                    help="allow more ranks than GPUs (ranks share cards round-robin): a rehearsal of the "
+                         "N > 1 path, flagged in the line, not a scaling measurement")
+    ap.add_argument("--allow-overrides", action="store_true",
+                    help="run even when an A/B kernel-selection variable (KERNEL_OVERRIDES) is set")
+    ap.add_argument("--plumbing-only", action="store_true",
+                    help="self-test of the multi-rank plumbing without a GPU: no kernel runs, the window "
+                         "times a host-side sleep; the line is marked as such")
     args = ap.parse_args()
+
+    # N ranks without a launcher: start them from here, before anything touches a GPU
+    if check_world(args.gpus) == "launch":
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    overrides = kernel_overrides()
+    if overrides and not args.allow_overrides and not args.plumbing_only:
+        raise SystemExit(f"bench.py: kernel-selection overrides set {overrides}; unset them or pass --allow-overrides")
 
     import torch
     import torch.distributed as dist
 
     world, rank, local = rank_info()
-    # one GPU per rank on the driver's node; a node with fewer devices than ranks (a rehearsal of the
-    # N > 1 path on one card) shares them round-robin (device_count() initialises nothing here)
-    local = local % max(torch.cuda.device_count(), 1)
+    if args.plumbing_only:
+        return plumbing_only(args, world, rank, dist)
+    # one GPU per rank (device_count() initialises nothing on this image)
+    ndev = torch.cuda.device_count()
+    local, shared = assign_device(local, world, ndev, args.rehearse_shared_devices)
     torch.cuda.set_device(local)             # before any other GPU call of this rank
     if world > 1:
         dist.init_process_group("gloo")
@@ -770,7 +912,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not shared else f"{METRIC} [REHEARSAL: {world} ranks shared {ndev} card(s)]",
             "value": value,
             "unit": "agent-steps/s",
             "n_gpus": world,
@@ -796,7 +938,11 @@ def main():
                                    "expiry inside it)"},
             },
             "binary": {"wh_version": _native.lib().wh_version().decode(), "source_sha": binary_sha,
-                       "tree_source_sha": source_sha(), "path": os.path.relpath(_native.LIB_PATH, ROOT)},
+                       "tree_source_sha": source_sha(), "path": os.path.relpath(_native.LIB_PATH, ROOT),
+                       "kernel_overrides": overrides},
+            "devices": {"physical_devices": ndev, "devices_shared": shared,
+                        "launch": "self-launched ranks" if os.environ.get("WH_BENCH_SELF_LAUNCHED") else
+                                  ("torch.distributed.run" if world > 1 else "single process")},
             "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,
             "desync_episodes": desync,

@@ -227,7 +227,11 @@ int wh_launch_run(const wh_launch* launch);
  * ends, so their span is the kernel's duration and no separate marker packets sit in the stream.
  * Either event may be NULL (e.g. start on the first of several launches, stop on the last). */
 int wh_launch_run_timed(const wh_launch* launch, void* start_event, void* stop_event);
-void wh_launch_free(wh_launch* launch);
+/* Frees a handle of wh_rollout_prepare.  Handles are tracked: run / run_timed / free of a pointer that
+ * is not a live handle (never prepared, or already freed) return WH_EINVAL and touch nothing, so a
+ * double free is refused instead of corrupting the heap.  NULL is a no-op (WH_OK).  A prepare with
+ * B = 0 needs no device and no tables: its handle launches nothing. */
+int wh_launch_free(wh_launch* launch);
 
 /* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a
  * ReLU MLP, hidden_layer_sizes [256,256] Small / [512,512] Medium / [1024,256] Large, 9 action

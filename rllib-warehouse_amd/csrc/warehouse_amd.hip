@@ -24,6 +24,7 @@
 
 #include <mutex>
 #include <type_traits>
+#include <unordered_set>
 #include <new>
 #include <stdint.h>
 #include <stdlib.h>
@@ -2462,6 +2463,8 @@ int prepare(const wh_config* cfg, int64_t B, void* stream, Geometry* g, const Ke
   if (B < 0) return WH_EINVAL;
   *kk = pick(*g);
   if (!*kk) return WH_ENOTSUP;
+  *tab = nullptr;
+  if (B == 0) return WH_OK;   // an empty batch launches nothing: no device, no tables
   return device_tables(*g, (*kk)->tblw, (hipStream_t)stream, tab);
 }
 
@@ -2599,6 +2602,15 @@ struct wh_launch {
   StepParams a;
 };
 
+// Live handles of wh_rollout_prepare: run / free of anything else (a freed or foreign pointer) is
+// refused with WH_EINVAL instead of being dereferenced.
+static std::mutex g_launch_mu;
+static std::unordered_set<const wh_launch*> g_launches;
+static bool launch_live(const wh_launch* l) {
+  std::lock_guard<std::mutex> lk(g_launch_mu);
+  return g_launches.count(l) != 0;
+}
+
 static int resolve_step(const wh_config* cfg, int64_t B, uint32_t* state, int policy, StepParams a,
                         void* stream, wh_launch* out) {
   Geometry g;
@@ -2735,14 +2747,18 @@ int wh_rollout_prepare(const wh_config* cfg, int64_t B, uint32_t* state, int32_t
     delete l;
     return rc;
   }
+  {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    g_launches.insert(l);
+  }
   *out = l;
   return WH_OK;
 }
 
-int wh_launch_run(const wh_launch* l) { return l ? enqueue(*l) : WH_EINVAL; }
+int wh_launch_run(const wh_launch* l) { return launch_live(l) ? enqueue(*l) : WH_EINVAL; }
 
 int wh_launch_run_timed(const wh_launch* l, void* start_event, void* stop_event) {
-  if (!l) return WH_EINVAL;
+  if (!launch_live(l)) return WH_EINVAL;
   if (l->a.B == 0) return WH_OK;
   StepParams a = l->a;
   void* args[] = {&a};
@@ -2750,7 +2766,15 @@ int wh_launch_run_timed(const wh_launch* l, void* start_event, void* stop_event)
                                     l->stream, (hipEvent_t)start_event, (hipEvent_t)stop_event, 0));
 }
 
-void wh_launch_free(wh_launch* l) { delete l; }
+int wh_launch_free(wh_launch* l) {
+  if (!l) return WH_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    if (!g_launches.erase(l)) return WH_EINVAL;   // not a live handle: never prepared, or freed already
+  }
+  delete l;
+  return WH_OK;
+}
 
 static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, float* obs, void* xfrag,
                         void* stream) {

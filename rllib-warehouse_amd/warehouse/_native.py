@@ -155,7 +155,7 @@ def lib() -> ctypes.CDLL:
     S.wh_launch_run.argtypes = [_P]
     S.wh_launch_run_timed.argtypes = [_P, _P, _P]
     S.wh_launch_free.argtypes = [_P]
-    S.wh_launch_free.restype = None
+    S.wh_launch_free.restype = ctypes.c_int
     for name in SYMBOLS:
         if name not in ("wh_version", "wh_launch_free") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int

@@ -41,6 +41,21 @@ def require_device(device=None) -> torch.device:
     return dev
 
 
+def _check_out(t, shape, dtype, device):
+    """A caller-supplied output tensor the kernel writes: exact shape, dtype and device, contiguous --
+    a tensor of the right shape but a narrower dtype, or on another GPU, would be written past its
+    end or into the wrong device's memory."""
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if t.dtype != dtype:
+        raise ValueError(f"expected dtype {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"expected a tensor on {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError("warehouse kernels take contiguous tensors")
+    return t
+
+
 def _dev_i32(x, device, shape=None):
     if x is None:
         return None
@@ -271,10 +286,7 @@ class BatchedWarehouse:
         dt = (torch.float32, torch.float32, torch.uint8)
         out = []
         for t, shape, d in zip((obs, rewards, dones), shapes, dt):
-            if t is None:
-                t = torch.empty(shape, dtype=d, device=self.device)
-            elif tuple(t.shape) != shape:
-                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+            t = torch.empty(shape, dtype=d, device=self.device) if t is None else _check_out(t, shape, d, self.device)
             out.append(t)
         self._call("wh_sampler_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
                    nat.ptr(out[1]), nat.ptr(out[2]), nat.ptr(out[0]),
@@ -291,10 +303,10 @@ class BatchedWarehouse:
                 returns=None, autoreset: bool = True) -> None:
         """`steps` fused iterations of {policy, step, auto-reset}.  rewards [steps,B,NA] float32,
         dones [steps,B] uint8 and returns [B] float32 (+=) are optional device tensors."""
-        for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
-                         (returns, (self.B,))):
-            if t is not None and tuple(t.shape) != shape:
-                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+        for t, shape, d in ((rewards, (steps, self.B, self.agent_slots), torch.float32),
+                            (dones, (steps, self.B), torch.uint8), (returns, (self.B,), torch.float32)):
+            if t is not None:
+                _check_out(t, shape, d, self.device)
         self._call("wh_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
                    nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
                    None if self.stats is None else self.stats.ref, int(bool(autoreset)),
@@ -319,10 +331,10 @@ class BatchedWarehouse:
         events=(start, stop) (torch.cuda.Event with enable_timing=True, either may be None): every
         launch stamps them at the kernel's own start and end (wh_launch_run_timed), so
         start.elapsed_time(stop) is the kernel's duration, with no marker packets around it."""
-        for t, shape in ((rewards, (steps, self.B, self.agent_slots)), (dones, (steps, self.B)),
-                         (returns, (self.B,))):
-            if t is not None and tuple(t.shape) != shape:
-                raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+        for t, shape, d in ((rewards, (steps, self.B, self.agent_slots), torch.float32),
+                            (dones, (steps, self.B), torch.uint8), (returns, (self.B,), torch.float32)):
+            if t is not None:
+                _check_out(t, shape, d, self.device)
         lib = nat.lib()
         handle = ctypes.c_void_p()
         nat.check(lib.wh_rollout_prepare(self._cfgp, self.B, self.state.data_ptr(), int(steps), POLICIES[policy],

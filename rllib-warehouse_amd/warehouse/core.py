@@ -172,6 +172,11 @@ class Warehouse(MultiAgentEnv):
 
     def step(self, action_dict: Dict[str, int]
              ) -> Tuple[Dict[str, dict], Dict[str, float], Dict[str, bool], Dict[str, dict]]:
+        """core.py:262-442 for one env.  Each dict entry moves its agent in iteration order; an agent
+        named under two key forms ('0' and 0, '-1' and str(n - 1)) moves once per entry.
+        Limit (not the reference's): at most `agent_slots` entries per dict -- the kernel's order row
+        is one entry per agent slot -- so a dict naming agents more times than that raises
+        ValueError, where the reference (core.py:279-281) would accept up to 4n key forms."""
         n, R = self._num_agents, self._num_requests
         h_io, d_io, h_regen, d_regen = self._io_buffers()
         io = h_io.numpy()                                    # row 0: actions, row 1: dict order

@@ -192,7 +192,9 @@ class WarehouseBaseEnv:
         Actions wrap like Python indexing; >= 9 raises IndexError (MOVES[action], core.py:281),
         and so does an agent id outside [-n, n) (agent_positions[idx], core.py:280); negative keys
         name agent n + key as numpy indexing does, and an agent named under two keys ('0' and 0)
-        moves once per entry with that entry's action (each order entry carries its own action)."""
+        moves once per entry with that entry's action (each order entry carries its own action).
+        Limit (not the reference's): at most NA entries per env dict (one order entry per agent
+        slot); more raise ValueError, where the reference would accept up to 4n key forms."""
         NA = self.vec.num_agents
         acts = np.full((self.num_envs, NA), 4, np.int32)
         order = np.full((self.num_envs, NA), -1, np.int32)

@@ -102,3 +102,76 @@ def test_two_rank_shards_equal_single_batch(tmp_path):
             ob.reset(L, S, d, mask=done)
     np.testing.assert_array_equal(sharded, S.pos)
     assert total == ref_total
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT") + bench_overrides()}
+    env.update(extra)
+    return env
+
+
+def bench_overrides():
+    import bench
+
+    return bench.KERNEL_OVERRIDES
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launches_n_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` with no torch.distributed.run around it starts both ranks itself (from
+    a parent that never touches a GPU), and rank 0 prints ONE line with n_gpus 2, the max-over-ranks
+    window and the host-core baseline.  --plumbing-only runs that path with no kernel (CPU here)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing-only",
+                        "--steps", "20", "--warmup", "5", "--cpu-procs", "1", "--cpu-seconds", "0.3"],
+                       cwd=root, env=_bench_env(), capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and "NOT A MEASUREMENT" in line["metric"]
+    assert line["config"]["launch"] == "self-launched ranks"
+    assert line["config"]["shard_offsets"] == [0, 65536]
+    assert line["ms_per_step"] * 20 >= 100.0          # the window is the slow rank's (0.1 s sleep)
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port"
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    import subprocess
+    import sys
+
+    import bench
+
+    assert bench.check_world(1, {}) == "run"
+    assert bench.check_world(8, {}) == "launch"
+    assert bench.check_world(8, {"WORLD_SIZE": "8"}) == "run"
+    with pytest.raises(SystemExit):
+        bench.check_world(2, {"WORLD_SIZE": "4"})
+    with pytest.raises(SystemExit):
+        bench.check_world(0, {})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing-only"],
+                       cwd=root, env=_bench_env(WORLD_SIZE="4", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE is 4" in r.stderr
+
+
+def test_bench_device_assignment_and_overrides():
+    import bench
+
+    assert bench.assign_device(3, 8, 8, False) == (3, False)
+    assert bench.assign_device(0, 1, 1, False) == (0, False)
+    with pytest.raises(SystemExit):
+        bench.assign_device(1, 2, 1, False)       # two ranks, one card: not a scaling run
+    assert bench.assign_device(1, 2, 1, True) == (0, True)
+    assert bench.assign_device(0, 2, 1, True) == (0, True)
+    with pytest.raises(SystemExit):
+        bench.assign_device(0, 1, 0, False)
+    assert bench.kernel_overrides({"WH_SAMPLER_UNFUSED": "1", "PATH": "x"}) == {"WH_SAMPLER_UNFUSED": "1"}
+    assert bench.kernel_overrides({}) == {}

@@ -575,6 +575,28 @@ def test_sampler_rollout_equals_sampler_steps(wh, variant, na, train, policy, p,
     np.testing.assert_array_equal(rew[K - 1].cpu().numpy()[ids], orew)
 
 
+
+def test_sampler_rollout_refuses_wrong_dtype_or_device(wh):
+    """Caller-supplied outputs of sampler_rollout / rollout must match the kernel's dtype and device
+    exactly: a float16 obs buffer of the right shape would be written past its end."""
+    import torch
+
+    env = wh.BatchedWarehouse("small", 64, 4, seed=3, device="cuda:0")
+    env.reset()
+    K, L = 2, env.obs_len
+    with pytest.raises(ValueError):
+        env.sampler_rollout(K, obs=torch.empty((K, 64, 4, L), dtype=torch.float16, device="cuda:0"))
+    with pytest.raises(ValueError):
+        env.sampler_rollout(K, rewards=torch.empty((K, 64, 4), dtype=torch.float32))   # host tensor
+    with pytest.raises(ValueError):
+        env.sampler_rollout(K, dones=torch.empty((K, 64), dtype=torch.int32, device="cuda:0"))
+    with pytest.raises(ValueError):
+        env.rollout(K, rewards=torch.empty((K, 64, 4), dtype=torch.bfloat16, device="cuda:0"))
+    with pytest.raises(ValueError):
+        env.rollout_launcher(K, dones=torch.empty((K, 64), dtype=torch.float32, device="cuda:0"))
+    obs, rew, dn = env.sampler_rollout(K)     # allocated by the env: accepted
+    assert obs.dtype == torch.float32 and dn.dtype == torch.uint8
+
 @pytest.mark.parametrize("variant,na,train,B,masked,ordered,stats", [
     ("medium", 8, False, 65536, False, False, False), ("medium", 8, False, 1000, True, True, True),
     ("small", 4, True, 2049, True, False, True), ("medium", 4, False, 513, False, True, False),
