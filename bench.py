@@ -455,11 +455,54 @@ def measure_sampler(env, K, W, dev, world, dist):
         kms = sorted(a.elapsed_time(b) / 20 for a, b in evs)
         return kms[len(kms) // 2]
 
-    split = {"k_sampler (fused: greedy + step + auto-reset + rows)": per_launch(one),
-             "two-launch form: k_step (1-step rollout)": per_launch(
-                 lambda: env.sampler_step("greedy", 0.0, observe=False)),
-             "two-launch form: k_observe": per_launch(env.observe)}
+    # the write ceiling of the rows: a plain fill_ of a buffer of the same size (the same bytes,
+    # streamed with nothing to compute), timed the same way
+    rows = torch.empty((env.B, env.agent_slots, env.obs_len), device=dev)
+    split = {"sampler_step": per_launch(one),
+             "step_only": per_launch(lambda: env.sampler_step("greedy", 0.0, observe=False)),
+             "observe_only": per_launch(env.observe),
+             "write_ceiling": per_launch(lambda: rows.fill_(1.0))}
+    del rows
     return elapsed, split
+
+
+def sampler_line(env, Ks, el, split, world, variant, words, fused):
+    """The bench line of the sampler route at env's shape (measure_sampler's numbers): throughput,
+    the per-launch split and the roofline of the launch that writes the rows.  fused: one k_sampler
+    launch per step (Medium-8); else the step launch + k_observe (configurations whose fused step
+    would spill at two waves per SIMD, Large-16)."""
+    B, NA = env.B, env.agent_slots
+    fms = split["sampler_step"]
+    rows_b = B * NA * env.obs_len * 4
+    # algorithmic bytes of a sampler step: rows written + packed state read and written (twice for
+    # the two-launch form: the observation launch reads it again) + rewards + dones
+    samp_b = rows_b + (2 if fused else 3) * B * 4 * words + B * (4 * NA + 1)
+    kname = "k_sampler" if fused else "k_step (1 step) + k_observe"
+    return {
+        "workload": f"RLlib sampler route, {variant} N={NA}, B={B}: device greedy policy + step + auto-reset + f32 "
+                    f"observation rows [B,{NA},{env.obs_len}] per step (wh_sampler_step -> "
+                    f"{'one k_sampler launch' if fused else 'k_step + k_observe'}); hipGraph of 100 steps",
+        "value": aggregate_rate(world, B, NA, Ks, el), "unit": "agent-steps/s", "steps": Ks,
+        "ms_per_step": el * 1e3 / Ks,
+        "kernel_split_ms": {
+            (f"{kname} (greedy + step + auto-reset + rows)"): fms,
+            "two-launch form: k_step (1-step rollout)": split["step_only"],
+            "two-launch form: k_observe": split["observe_only"],
+            f"write ceiling: torch fill_ of the same {rows_b / 1e6:.1f} MB": split["write_ceiling"]},
+        "two_launch_form_ms": split["step_only"] + split["observe_only"],
+        # what the step costs on top of streaming the same rows: the sampler launch minus a plain
+        # write of the same bytes (and, for comparison, minus k_observe, which also builds the rows)
+        "step_share_ms": fms - split["write_ceiling"],
+        "step_share_vs_observe_ms": fms - split["observe_only"],
+        "roofline": {"bound": "hbm", "kernel": kname, "kernel_ms": fms,
+                     "bytes_per_launch": samp_b, "achieved": samp_b / (fms * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": samp_b / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "write_ceiling_frac": rows_b / (split["write_ceiling"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "note": "algorithmic bytes = B*NA*(9R+1)*4 rows + packed state (read + write, + a second "
+                             "read for the two-launch form) + rewards + dones; write_ceiling_frac = the rows' bytes "
+                             "/ the fill_ time / 8 TB/s"},
+    }
 
 
 def measure_sampler_rollout(env, K, frag, W, dev, world, dist):
@@ -628,6 +671,17 @@ def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     torch.cuda.synchronize(dev)
     kms = sorted(a.elapsed_time(b) / 5 for a, b in evs)
     return elapsed, kms[len(kms) // 2], net
+
+
+def mlp_kernel_name(net, prec):
+    """The policy kernel wh_mlp_forward dispatches for this network (policy_mlp.hip find_mlp): the
+    exact-f32 kernel, or bf16 on 16x16x32 tiles (k_mlp16) for the Medium and Large shapes, else the
+    32x32x16 kernel (k_mlp)."""
+    if prec != "bf16":
+        return "k_mlp_f32"
+    if (net.in_dim, net.hidden[0], net.hidden[1]) in ((82, 512, 512), (145, 1024, 256)):
+        return "k_mlp16 (v_mfma_f32_16x16x32_bf16)"
+    return "k_mlp (v_mfma_f32_32x32x16_bf16)"
 
 
 def step_roofline(m, variant, NA, policy, mode):
@@ -821,33 +875,25 @@ def main():
         # not one graph launch's host latency over a 20-step window)
         Ks = max(min(K, 1000), 200)
         el3, split = measure_sampler(env, Ks, W, dev, world, dist)
-        fms = split["k_sampler (fused: greedy + step + auto-reset + rows)"]
-        # algorithmic bytes of the fused launch: rows written + packed state read and written +
-        # rewards + dones
-        samp_b = B * NA * env.obs_len * 4 + 2 * B * 4 * words + B * (4 * NA + 1)
+        sampler = sampler_line(env, Ks, el3, split, world, args.variant, words, fused=True)
+        sampler["roofline"]["traffic"] = load_traffic(f"{args.variant}_n{NA}_sampler")
         el5, Kpp = measure_sampler_pipeline(env, Ks, W, dev, world, dist)
-        sampler = {
-            "workload": f"RLlib sampler route: device greedy policy + step + auto-reset + f32 observation rows "
-                        f"[B,{NA},{env.obs_len}] in one launch (wh_sampler_step -> k_sampler); hipGraph of 100 steps",
-            "value": aggregate_rate(world, B, NA, Ks, el3), "unit": "agent-steps/s", "steps": Ks,
-            "ms_per_step": el3 * 1e3 / Ks,
-            "kernel_split_ms": split,
-            "two_launch_form_ms": split["two-launch form: k_step (1-step rollout)"] + split["two-launch form: k_observe"],
-            # what the step adds to a launch that writes the same rows: the fused launch minus the
-            # row-writing kernel alone (k_observe: same rows, same state read, no step)
-            "step_share_ms": fms - split["two-launch form: k_observe"],
-            "two_stream_pipeline": {
-                "workload": "the two-launch form as SamplerPipeline: the rows of step s on a side stream while "
-                            "step s+1 runs (state double-buffered); slower -- the step launch's workgroups only "
-                            "start as the observation kernel's drain (DESIGN.md §5)",
-                "value": aggregate_rate(world, B, NA, Kpp, el5), "steps": Kpp, "ms_per_step": el5 * 1e3 / Kpp},
-            "roofline": {"bound": "hbm", "kernel": "k_sampler", "kernel_ms": fms,
-                         "bytes_per_launch": samp_b, "achieved": samp_b / (fms * 1e-3) / 1e9,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": samp_b / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": load_traffic(f"{args.variant}_n{NA}_sampler"),
-                         "note": "algorithmic bytes = B*NA*(9R+1)*4 rows + 2 x packed state + rewards + dones"},
-        }
+        sampler["two_stream_pipeline"] = {
+            "workload": "the two-launch form as SamplerPipeline: the rows of step s on a side stream while "
+                        "step s+1 runs (state double-buffered); slower -- the step launch's workgroups only "
+                        "start as the observation kernel's drain (DESIGN.md §5)",
+            "value": aggregate_rate(world, B, NA, Kpp, el5), "steps": Kpp, "ms_per_step": el5 * 1e3 / Kpp}
+
+    # C4's shape on the same route (BASELINE config 4: Large, 16 agents, B = 65,536): its step code
+    # needs 360 registers, so the fused k_sampler (two waves per SIMD, 256 registers) would spill and
+    # the route takes the step launch + k_observe
+    sampler_c4 = None
+    if not args.no_sampler and (args.variant, NA, B) == ("medium", 8, 65536):
+        env4 = warehouse.BatchedWarehouse("large", B, 16, seed=1234, env_offset=shard_offset(rank, B), device=dev)
+        env4.reset()
+        el8, split8 = measure_sampler(env4, 200, W, dev, world, dist)
+        sampler_c4 = sampler_line(env4, 200, el8, split8, world, "large", env4.layout.words_per_env, fused=False)
+        del env4
 
     fragment = None
     if not args.no_sampler:
@@ -900,7 +946,7 @@ def main():
                 "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,
                 "ms_per_step": el4 * 1e3 / Kp,
                 "dtype": "bf16 MFMA, f32 accumulate" if prec == "bf16" else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
-                "roofline": {"bound": "mfma", "kernel": "k_mlp" if prec == "bf16" else "k_mlp_f32", "kernel_ms": mms,
+                "roofline": {"bound": "mfma", "kernel": mlp_kernel_name(net, prec), "kernel_ms": mms,
                              "flop_per_launch": flop, "achieved": flop / (mms * 1e-3) / 1e12, "peak": peak,
                              "unit": "TFLOP/s", "frac": flop / (mms * 1e-3) / 1e12 / peak,
                              "traffic": load_traffic(f"{args.variant}_n{NA}_mlp" + ("" if prec == "bf16" else "_f32"))},
@@ -947,6 +993,7 @@ def main():
             "alt_launch_mode": alt,
             "desync_episodes": desync,
             "sampler_path": sampler,
+            "sampler_path_c4": sampler_c4,
             "sampler_fragments": fragment,
             "vector_path": vector,
             "policy_path": policy_line,

@@ -78,17 +78,44 @@ constexpr bool kRegenHoist = true;
 #else
 constexpr bool kRegenHoist = false;
 #endif
+// Regeneration targets of items 1 and 2 by skipping the earlier items' targets (a compare-add each)
+// instead of a rank selection on a used-target mask; the mask is built only from item 3 on.  Same
+// values.  -DWH_NO_REGEN_SKIP: the mask for every item (A/B).
+// -DWH_HOIST_POLICY: the regeneration's first Philox block computed at the top of the fused step,
+// in the policy's basic block (its ten rounds then fill the gaps around the request-table reads)
+// instead of inside the move loop's (A/B).
+#ifdef WH_HOIST_POLICY
+constexpr bool kHoistPolicy = true;
+#else
+constexpr bool kHoistPolicy = false;
+#endif
+#ifndef WH_NO_REGEN_SKIP
+constexpr bool kRegenSkip = true;
+#else
+constexpr bool kRegenSkip = false;
+#endif
 
 constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle agent
 constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
+
+// Cell -> pickup table (u8 per cell).  Default: byte x | y << 8 (one v_perm of the packed position);
+// its dword -- the LDS bank -- is x >> 2, so every lane of a wave reads one of D/4 banks (~8-way
+// conflicts).  -DWH_CELL_SKEW: byte 4x + 132y (one v_dot2 of the masked position), bank (x + y) mod 32.
+#ifdef WH_CELL_SKEW
+constexpr bool kCellSkew = true;
+#else
+constexpr bool kCellSkew = false;
+#endif
+__host__ __device__ constexpr int cell_bytes(int D) { return kCellSkew ? 132 * D : 256 * D; }
+__host__ __device__ constexpr int cell_index(int x, int y) { return kCellSkew ? 4 * x + 132 * y : (x | (y << 8)); }
 
 // Shared (per-workgroup) table layout in bytes; built identically by build_tables() on the host.
 struct TableLayout {
   int cell, rp, tag, dst, mv, valid, bytes;
   __host__ __device__ constexpr TableLayout(int D, int P, int DP, int NV)
-      : cell(0), rp(256 * D), tag(256 * D + 4), dst(256 * D + 8 * (P + 1)),   // rp/tag interleaved
-        mv(256 * D + 8 * (P + 1) + 4 * DP), valid(256 * D + 8 * (P + 1) + 4 * DP + 48),
-        bytes(256 * D + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
+      : cell(0), rp(cell_bytes(D)), tag(cell_bytes(D) + 4), dst(cell_bytes(D) + 8 * (P + 1)),   // rp/tag interleaved
+        mv(cell_bytes(D) + 8 * (P + 1) + 4 * DP), valid(cell_bytes(D) + 8 * (P + 1) + 4 * DP + 48),
+        bytes(cell_bytes(D) + 8 * (P + 1) + 4 * DP + 48 + 4 * NV) {}
 };
 
 template <int D_, int R_, int NR_, int NAM_>
@@ -161,6 +188,10 @@ __device__ __forceinline__ uint32_t sgn(uint32_t x) {
   asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
   return r;
 }
+// The same sign mask as v_bfe_i32 x, 31, 1 through the builtin: no inline asm, so the hazard
+// recognizer does not pad the next VALU with an s_nop (select_bit64 chains five of them per call);
+// where LLVM would rewrite it into a compare (a difference of two values) the asm form stays.
+__device__ __forceinline__ uint32_t sgn_bfe(uint32_t x) { return (uint32_t)__builtin_amdgcn_sbfe((int)x, 31u, 1u); }
 __device__ __forceinline__ uint32_t mask_z(uint32_t x) { return sgn(x - 1u); }   // x == 0 (x < 2^31)
 __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { return bop3<(TA & TB) | (~TA & TC)>(m, a, b); }
 
@@ -170,7 +201,7 @@ __device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t a, uint32_t b) { r
 __device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
   uint32_t sr = ~r;
   uint32_t u = (uint32_t)__popc((uint32_t)m) + sr;
-  uint32_t g = sgn(u);
+  uint32_t g = sgn_bfe(u);
   uint32_t w = msel(g, (uint32_t)(m >> 32), (uint32_t)m);
   sr = msel(g, u, sr);
   const uint32_t half = bop3<TA & TB>(g, 32u, 0u);
@@ -179,7 +210,7 @@ __device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
 #pragma unroll
   for (int k = 16; k >= 1; k >>= 1) {
     u = (uint32_t)__popc(__builtin_amdgcn_ubfe(w, base, (uint32_t)k)) + sr;
-    g = sgn(u);
+    g = sgn_bfe(u);
     if (k > 1) sr = msel(g, u, sr);
     base = bop3<(TA & TB) | TC>(g, (uint32_t)k, base);
   }
@@ -246,6 +277,15 @@ __device__ __forceinline__ uint32_t action_of(uint32_t d) {
   return (uint32_t)(3 * ((int)v.x + 1) + ((int)v.y + 1));
 }
 
+// Rare wave-uniform branches of the step loop (expiry pass, grid rebuild, resets, random moves): marked
+// cold so that block placement keeps their code out of the hot path's instruction stream.
+// -DWH_NO_COLD: no annotation (A/B).
+#ifndef WH_NO_COLD
+#define WH_RARE(x) __builtin_expect(!!(x), 0)
+#else
+#define WH_RARE(x) (x)
+#endif
+
 // Phase labels in the device assembly for instruction-count analysis; -DWH_NO_PHASE_MARKS drops them.
 #ifndef WH_NO_PHASE_MARKS
 #define WH_PHASE_MARK(name) asm volatile("; PHASE " #name ::: "memory")
@@ -278,7 +318,13 @@ struct Lds {
   // Cell (x | y << 16) -> pickup index + 1, 0 for other cells: one v_perm (the byte index
   // x | y << 8) + one ds_read_u8; the point's row in pkp is then one v_lshl_add away (row_byte).
   __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
-    return reinterpret_cast<const uint8_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
+    if constexpr (kCellSkew) {
+      typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+      const uint32_t i = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, xy16 & XY16), (u16x2){4, 132}, 0u, false);
+      return reinterpret_cast<const uint8_t*>(tbl)[i];
+    } else {
+      return reinterpret_cast<const uint8_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
+    }
   }
 
   // (pickup cell, greedy tag) of point j: one 8-byte LDS read
@@ -326,18 +372,33 @@ struct NoSlots {};
 // Every 16-byte load of a lane is issued before its first LDS write, so the prologue pays one
 // memory round trip.  (A strided `for` loop over words compiled to load -> vmcnt(0) -> ds_write per
 // iteration: ~10 serial round trips per launch at Medium-8, most of a short launch's fixed cost.)
+// Split in two: issue_tables() puts the loads in flight first (the table is L2-resident: it comes back
+// well before the state planes from HBM), commit_tables() writes them to LDS -- the waitcnt pass then
+// waits for the table loads only (vmcnt counts in order), with the state loads still in flight.
+// Chunk i (16 bytes per lane) of the table, as plain values: a struct or array of them crossing
+// the state loads was kept in memory by LLVM (promoted to LDS, 32 bytes per lane, or put in scratch).
+template <class C>
+constexpr int kTableChunks = (C::TBL4 + BT - 1) / BT;
+template <class C>
+__device__ __forceinline__ bool table_lane(int i) {
+  return i < kTableChunks<C> && (C::TBL4 % BT == 0 || i + 1 < kTableChunks<C> || (int)threadIdx.x + i * BT < C::TBL4);
+}
+template <class C>
+__device__ __forceinline__ uint4 issue_table_chunk(const uint32_t* __restrict__ tables, int i) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (table_lane<C>(i)) v = reinterpret_cast<const uint4*>(tables)[threadIdx.x + i * BT];
+  return v;
+}
+template <class C>
+__device__ __forceinline__ void commit_table_chunk(uint32_t* dst, int i, uint4 v) {
+  if (table_lane<C>(i)) reinterpret_cast<uint4*>(dst)[threadIdx.x + i * BT] = v;
+}
 template <class C>
 __device__ __forceinline__ void load_tables(uint32_t* dst, const uint32_t* __restrict__ tables) {
-  constexpr int IT = (C::TBL4 + BT - 1) / BT;
-  const uint4* src = reinterpret_cast<const uint4*>(tables);
-  uint4* d4 = reinterpret_cast<uint4*>(dst);
-  uint4 v[IT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i)
-    if (C::TBL4 % BT == 0 || i + 1 < IT || (int)threadIdx.x + i * BT < C::TBL4) v[i] = src[threadIdx.x + i * BT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i)
-    if (C::TBL4 % BT == 0 || i + 1 < IT || (int)threadIdx.x + i * BT < C::TBL4) d4[threadIdx.x + i * BT] = v[i];
+  static_assert(kTableChunks<C> <= 2, "tables of at most 2 x 4 KB");
+  const uint4 v0 = issue_table_chunk<C>(tables, 0), v1 = issue_table_chunk<C>(tables, 1);
+  commit_table_chunk<C>(dst, 0, v0);
+  commit_table_chunk<C>(dst, 1, v1);
 }
 
 template <class C>
@@ -353,9 +414,13 @@ __device__ __forceinline__ uint64_t low_mask() {
   return N >= 64 ? ~0ull : ((1ull << N) - 1ull);
 }
 
-// The packed words of one env, loaded to registers.  Issued before the workgroup's table load so
-// the two memory latencies of the prologue overlap (vmcnt retires in order: the table wait covers
-// these loads too).
+// The packed words of one env, loaded to registers.  Word plane w of the workgroup's envs is
+// st + w * B + e0 (e0 = the workgroup's first env): a wave-uniform pointer, advanced by B with two
+// scalar adds per plane, and the lane's offset tid * 4 -- global loads in SGPR-base form, so no
+// per-lane 64-bit address arithmetic (it was ~100 VALU, a third of them v_mad_u64_u32, in front of
+// the first load).  Issue order = use order: the header and the pickup planes (target, expiry
+// pairs: the pickup plane is built from them while the rest arrive), then the episode counter and
+// the agent words (first used in the step loop).
 template <class C>
 struct RawEnv {
   uint32_t hdr, epi, ag[C::NAM], pt[C::PW], pm[C::PW];
@@ -363,16 +428,25 @@ struct RawEnv {
 
 template <class C>
 __device__ __forceinline__ void load_env_issue(RawEnv<C>& r, const uint32_t* __restrict__ st, int64_t B,
-                                               int64_t e, int na) {
-  r.hdr = st[e];
-  r.epi = st[B + e];
+                                               int64_t e0, int tid, int na) {
+  const uint32_t* pl = st + e0;
+  r.hdr = pl[tid];
+  const uint32_t* pt = pl + (int64_t)(2 + na) * B;
+  const uint32_t* pm = pt + (int64_t)C::PW * B;
 #pragma unroll
-  for (int i = 0; i < C::NAM; ++i) r.ag[i] = (i < na) ? st[(2 + i) * B + e] : IDLE;
-  const int wpt = 2 + na;
+  for (int w = 0; w < C::PW; ++w) {
+    r.pt[w] = pt[tid];
+    r.pm[w] = pm[tid];
+    pt += B;
+    pm += B;
+  }
+  pl += B;
+  r.epi = pl[tid];
 #pragma unroll
-  for (int w = 0; w < C::PW; ++w) r.pt[w] = st[(wpt + w) * B + e];
-#pragma unroll
-  for (int w = 0; w < C::PW; ++w) r.pm[w] = st[(wpt + C::PW + w) * B + e];
+  for (int i = 0; i < C::NAM; ++i) {
+    pl += B;
+    r.ag[i] = (i < na) ? pl[tid] : IDLE;
+  }
 }
 
 // SWAR byte ops on 4 packed unsigned bytes (H = the bytes' high bits)
@@ -415,20 +489,28 @@ __device__ __forceinline__ void load_env_finish(Regs<C>& s, Lds<C>& L, const Raw
 
 template <class C>
 __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uint32_t* __restrict__ st,
-                                          int64_t B, int64_t e, int na, int tid) {
-  st[e] = s.hdr;
-  st[B + e] = s.epi;
+                                          int64_t B, int64_t e0, int na, int tid) {
+  uint32_t* pl = st + e0;   // word planes as in load_env_issue: wave-uniform base + lane offset
+  pl[tid] = s.hdr;
+  pl += B;
+  pl[tid] = s.epi;
 #pragma unroll
   for (int i = 0; i < C::NAM; ++i)
-    if (i < na) st[(2 + i) * B + e] = s.ag[i];
-  const int wpt = 2 + na;
+    if (i < na) {
+      pl += B;
+      pl[tid] = s.ag[i];
+    }
+  uint32_t* pt = pl + B;
+  uint32_t* pm = pt + (int64_t)C::PW * B;
 #pragma unroll
   for (int w = 0; w < C::PW; ++w) {
     // four 16-bit cells -> target bytes and expiry bytes: two shift-ors and two v_perm
     const uint32_t lo = (uint32_t)L.pkp[4 * w][tid] | ((uint32_t)L.pkp[4 * w + 1][tid] << 16);
     const uint32_t hi = (uint32_t)L.pkp[4 * w + 2][tid] | ((uint32_t)L.pkp[4 * w + 3][tid] << 16);
-    st[(wpt + w) * B + e] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
-    st[(wpt + C::PW + w) * B + e] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
+    pt[tid] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+    pm[tid] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
+    pt += B;
+    pm += B;
   }
 }
 
@@ -708,7 +790,7 @@ __device__ __forceinline__ void policy_steps(const Regs<C>& s, const Lds<C>& L, 
       // goal is a grid cell, so pos + d stays on the grid: step_env<CLAMP = false> adds it as is
       d[i] = pk_min_i16(pk_max_i16(pk_sub_i16(goal, pos), 0xFFFFFFFFu), 0x00010001u);
     }
-    if (p > 0.0f) {
+    if (WH_RARE(p > 0.0f)) {
 #pragma unroll
       for (int b = 0; b < (C::NAM + 1) / 2; ++b) {
         const uint4 blk = stream_block(k, gid, s.epi, t, PUR_POLICY, (uint32_t)b);
@@ -755,13 +837,18 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
                                          const int32_t* __restrict__ regen, const Keys& k,
                                          uint32_t gid, int64_t e, int na, int phase, uint32_t T,
                                          uint32_t W, float (&rew)[C::NAM], int32_t* n_inactive,
-                                         int tid, int ablate, LazyGrid* lg = nullptr) {
+                                         int tid, int ablate, LazyGrid* lg = nullptr,
+                                         const uint4* pre_rblk = nullptr) {
   const uint32_t n = (s.hdr >> 16) & 0xFFu;
   uint32_t t = s.hdr & 0xFFFFu;
   uint32_t rewm[C::NAM];   // reward masks: all-ones = 1.0f
-  constexpr bool HOIST = LAZY && !INJ && kRegenHoist;   // (see the move phase)
+  constexpr bool HOIST = LAZY && !INJ && kRegenHoist && !kHoistPolicy;   // (see the move phase)
   uint4 rblk0 = make_uint4(0u, 0u, 0u, 0u);
   bool hoisted = false;
+  if (pre_rblk) {   // computed by the caller ahead of the policy (kHoistPolicy)
+    rblk0 = *pre_rblk;
+    hoisted = true;
+  }
 
   if (phase != PH_REGEN) {
     t = (t + 1u) & 0xFFFFu;                                 // core.py:267
@@ -778,7 +865,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     //      which lets its lookups be issued inside it.
     WH_PHASE_MARK(expire);
     const uint64_t em = (ablate & 4) ? 0ull : __ballot(t >= s.wskip);
-    if (em && __popcll(em) == 1 && __ballot(true) == ~0ull) {
+    if (WH_RARE(em != 0) && __popcll(em) == 1 && __ballot(true) == ~0ull) {
       // one lane of a full wave due (desynchronised episodes): its P pickup cells checked one per
       // lane of the wave, instead of the whole wave walking every lane's requests
       const int l = __builtin_ctzll(em), lane = tid & 63, col = (tid & ~63) + l;
@@ -788,7 +875,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       if (ex) L.clear_target(lane, col);
       const uint64_t exm = __ballot(ex);
       s.am = lane == l ? (s.am & ~exm) : s.am;
-    } else if (em) {
+    } else if (WH_RARE(em != 0)) {
       if (__any(__popcll(s.am) > C::R)) {   // a hand-built state with more than R requests: scan all
         uint64_t expired = 0;
 #pragma unroll
@@ -884,7 +971,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           const uint32_t mlive = sgn((uint32_t)i - n);
           atomicOr(&L.occ[p >> 16][tid], bop3<TA & TB>(mlive, 1u << (p & 31u), 0u));
         }
-      } else if (__any(lg->rebuild)) {
+      } else if (WH_RARE(__any(lg->rebuild))) {
         // (the terms are written so that none is shared with the move loop below: a shared one
         // would be hoisted above the branch, and the skip path would pay a register copy per term)
         const uint32_t livebits = (2u << (n - 1u)) - 1u;   // n >= 1
@@ -1079,7 +1166,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #ifdef WH_FORCE_NOREV   // timing-only A/B builds: never the reverse-key loop (wrong with co-located agents)
         if (!LAZY && !UKEY)
 #else
-        if (!UKEY && (!LAZY || C::NAM > kRevSplitMaxNam || __any(lg->cm != 0u)))
+        if (!UKEY && (!LAZY || C::NAM > kRevSplitMaxNam || WH_RARE(__any(lg->cm != 0u))))
 #endif
         {
 #ifdef WH_COUNT_REV   // A/B builds: count the wave-steps that take the reverse-key loop (wh_check_read)
@@ -1100,7 +1187,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           for (int i = (C::NAM > 3 ? C::NAM - 3 : 0); i < C::NAM; ++i) pick(i, cp[i], tb[i], dst[i]);
         }
         looked = true;
-        if (LAZY && __any(lg->cm != 0u)) {   // did an agent that shares a cell move?
+        if (LAZY && WH_RARE(__any(lg->cm != 0u))) {   // did an agent that shares a cell move?
           uint32_t acc = 0;
 #pragma unroll
           for (int i = 0; i < C::NAM; ++i)
@@ -1150,6 +1237,7 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
       uint32_t rlo = (uint32_t)inactive, rhi = (uint32_t)(inactive >> 32);   // still selectable
       uint32_t ulo = 0, uhi = 0;                                               // targets used
       uint32_t olo = 0, ohi = 0;                                               // points opened
+      uint32_t tj[3] = {0u, 0u, 0u};   // targets of items 0-2 (kRegenSkip)
       uint32_t first_t = 0;
       const uint32_t wexp = ((t + W) & 0xFFu) << 8;   // expires at step t + W
       uint4 blk = make_uint4(0u, 0u, 0u, 0u);   // words 2j (pickup) and 2j+1 (target) share a block
@@ -1168,14 +1256,31 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             ma = bop3<TA & TB>(ma, 0u - (uint32_t)valid, 0u);
             sel = select_bit64(inactive, rpos);   // positions into the inactive list, host-drawn
           } else {
-            if ((j & 1) == 0) blk = (HOIST && j == 0 && hoisted) ? rblk0 : stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
+            if ((j & 1) == 0) blk = ((HOIST || kHoistPolicy) && j == 0 && hoisted) ? rblk0 : stream_block(k, gid, s.epi, t, PUR_REGEN, (uint32_t)(j >> 1));
             const uint32_t w1 = comp(blk, (2 * j) & 3), w2 = comp(blk, (2 * j + 1) & 3);
             sel = select_bit64(((uint64_t)rhi << 32) | rlo, __umulhi(w1, nin - (uint32_t)j));
             const uint32_t r2 = __umulhi(w2, (uint32_t)(C::DP - j));
             if (j == 0) tgi = r2;                                               // nothing used yet
             else if (j == 1) tgi = r2 + ((first_t - 1u - r2) >> 31);   // + (r2 >= first): skip it
-            else tgi = select_bit64(~(((uint64_t)uhi << 32) | ulo) & low_mask<C::DP>(), r2);
+            else if (kRegenSkip && j == 2) {
+              // the r2-th target not used by items 0 and 1: skip each of them at or below it, in
+              // ascending order (the same value as the rank selection on the used mask)
+              const uint32_t lo = min(tj[0], tj[1]), hi = max(tj[0], tj[1]);
+              tgi = r2 + ((lo - 1u - r2) >> 31);
+              tgi += (hi - 1u - tgi) >> 31;
+            } else {
+              if (kRegenSkip && j == 3) {   // from item 3 on: the used mask, built from items 0-2
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                  const uint64_t b = 1ull << (tj[q] & 63u);
+                  ulo |= (uint32_t)b;
+                  uhi |= (uint32_t)(b >> 32);
+                }
+              }
+              tgi = select_bit64(~(((uint64_t)uhi << 32) | ulo) & low_mask<C::DP>(), r2);
+            }
             if (j == 0) first_t = r2;
+            if (j < 3) tj[j] = tgi;
           }
           const uint64_t sb = 1ull << (sel & 63u), tb64 = 1ull << (tgi & 63u);
           const uint32_t slo = bop3<TA & TB>(ma, (uint32_t)sb, 0u), shi = bop3<TA & TB>(ma, (uint32_t)(sb >> 32), 0u);
@@ -1183,8 +1288,10 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           rhi &= ~shi;
           olo |= slo;
           ohi |= shi;
-          ulo = bop3<(TA & TB) | TC>(ma, (uint32_t)tb64, ulo);
-          uhi = bop3<(TA & TB) | TC>(ma, (uint32_t)(tb64 >> 32), uhi);
+          if (!kRegenSkip || j >= 3) {   // (kRegenSkip: items 0-2 skip their targets arithmetically)
+            ulo = bop3<(TA & TB) | TC>(ma, (uint32_t)tb64, ulo);
+            uhi = bop3<(TA & TB) | TC>(ma, (uint32_t)(tb64 >> 32), uhi);
+          }
           // predicated store: lanes with nothing to open write the scratch row
           L.pkp[msel(ma, sel, (uint32_t)C::P)][tid] = (uint16_t)((tgi + 1u) | wexp);
         }
@@ -1198,17 +1305,24 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
   if (phase != PH_REGEN) {
     // ---- deliveries (core.py:354-368): target cell == position (idle agents never match)
     WH_PHASE_MARK(deliver);
+    // Manhattan distance position -> target cell minus 1 is ONE v_sad_u8 of the agent word against
+    // its target bytes doubled ([x, dx, y, dy] vs [dx, dx, dy, dy], accumulator -1): negative exactly
+    // when the agent stands on its target (an idle agent's 0xFF bytes never match).  The reward of
+    // the pickup or the delivery is folded into the same bitop3 that makes the 1.0f.
+    uint32_t delm[C::NAM];
+#pragma unroll
+    for (int i = 0; i < C::NAM; ++i) delm[i] = 0u;
     if (!(ablate & 32)) {
 #pragma unroll
       for (int i = 0; i < C::NAM; ++i) {
         const uint32_t a = s.ag[i];
-        const uint32_t m = mask_z(bop3<(TA ^ TB) & TC>(a >> 8, a, XY16));   // target cell == position
+        const uint32_t m = sgn(__builtin_amdgcn_sad_u8(a, __builtin_amdgcn_perm(a, a, 0x03030101u), 0xFFFFFFFFu));
         s.ag[i] = bop3<(TA & TB) | TC>(m, IDLE, a);
-        rewm[i] |= m;   // a pickup (interior cell) and a delivery (border cell) never share a step
+        delm[i] = m;   // a pickup (interior cell) and a delivery (border cell) never share a step
       }
     }
 #pragma unroll
-    for (int i = 0; i < C::NAM; ++i) rew[i] = __uint_as_float(bop3<TA & TB>(rewm[i], 0x3F800000u, 0u));
+    for (int i = 0; i < C::NAM; ++i) rew[i] = __uint_as_float(bop3<(TA | TB) & TC>(rewm[i], delm[i], 0x3F800000u));
     WH_PHASE_MARK(tail);
     done = t >= T;                                            // core.py:438
     s.hdr = t | (n << 16);                                    // clears `fresh`
@@ -1558,7 +1672,7 @@ struct FastRun {
     }
     rrow += rstride;
     drow += a.B;
-    if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
+    if (!(ablate & 128) && WH_RARE(__any(done))) {   // wave-uniform test first: one branch on the common path
       const uint64_t dm = __ballot(done);
       // a few envs of a full wave end (desynchronised episodes): wave-wide resets of them, one env
       // at a time (every lane takes part, so not in a tail wave whose lanes past B have exited)
@@ -1601,8 +1715,9 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
 #else
   constexpr int ablate = 0;
 #endif
-  float* rrow = a.rewards + e * C::NAM;
-  uint8_t* drow = a.dones + e;
+  // output rows of step stp: wave-uniform bases (scalar adds per step) + the lane's offset
+  float* rrow = a.rewards + (e - tid) * C::NAM;
+  uint8_t* drow = a.dones + (e - tid);
   const int64_t rstride = a.B * C::NAM;
   LazyGrid lg{true, 0u};   // the grid starts empty (k_step)
   for (int stp = 0; stp < a.steps; ++stp) {
@@ -1619,16 +1734,22 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
     } else {
       policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
+    uint4 rb = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (kHoistPolicy) {   // pinned to the policy's block (LLVM would sink it to its use)
+      rb = stream_block(k, gid, s.epi, (s.hdr + 1u) & 0xFFFFu, PUR_REGEN, 0u);
+      asm volatile("" : "+v"(rb.x), "+v"(rb.y), "+v"(rb.z), "+v"(rb.w));
+    }
     float rew[C::NAM];
     const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
-                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg);
+                                                (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg,
+                                                kHoistPolicy ? &rb : nullptr);
     if (!(ablate & 64)) {
-      store_row<C>(rrow, rew);
-      *drow = done ? 1 : 0;
+      store_row<C>(rrow + tid * C::NAM, rew);
+      drow[tid] = done ? 1 : 0;
     }
     rrow += rstride;
     drow += a.B;
-    if (!(ablate & 128) && __any(done)) {   // wave-uniform test first: one branch on the common path
+    if (!(ablate & 128) && WH_RARE(__any(done))) {   // wave-uniform test first: one branch on the common path
       const uint64_t dm = __ballot(done);
       // a few envs of a full wave end (desynchronised episodes): wave-wide resets of them, one env
       // at a time (every lane takes part, so not in a tail wave whose lanes past B have exited)
@@ -1687,9 +1808,20 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
   const bool live = e < a.B && (FAST || !a.mask || a.mask[e]);
   const int na = FAST ? C::NAM : a.na;   // the fast instance runs na == NAM only (resolve_step)
+  const int64_t e0 = (int64_t)blockIdx.x * BT;
+  // Prologue: the table loads (L2) first, then the state planes (HBM); the table is written to LDS
+  // and the occupancy grid cleared while the state is still in flight, and the pickup plane is
+  // built as the state words land (the waitcnt pass counts each use against the in-order vmcnt).
+  const uint4 tv0 = issue_table_chunk<C>(a.tables, 0), tv1 = issue_table_chunk<C>(a.tables, 1);
+  __builtin_amdgcn_sched_barrier(0);   // keep the table loads ahead of the state loads
+  // every lane loads (a lane past B or masked out re-reads env e0, which exists): a load under an exec
+  // branch would make the waitcnt pass drain the state loads before the table's LDS writes
   RawEnv<C> raw;
-  if (live) load_env_issue<C>(raw, a.state, a.B, e, na);
-  load_tables<C>(L.tbl, a.tables);
+  load_env_issue<C>(raw, a.state, a.B, e0, live ? tid : 0, na);
+  commit_table_chunk<C>(L.tbl, 0, tv0);
+  commit_table_chunk<C>(L.tbl, 1, tv1);
+#pragma unroll
+  for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
   __syncthreads();
   if (FAST) WH_T(1);
   if (!live) return;
@@ -1705,8 +1837,6 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   // waitcnt pass places vmcnt waits in the loop body, where on every later iteration they also
   // wait for the previous step's reward/done stores to retire (a full memory round trip per step).
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding)
-#pragma unroll
-  for (int y = 0; y < C::D; ++y) L.occ[y][tid] = 0u;   // occupancy grid starts empty (step_env)
   if constexpr (FAST) RS.rs_ep[tid] = s.epi;            // reset slots start stale (!= epi + 1)
   if (FAST) WH_T(2);
 
@@ -1727,7 +1857,7 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
   if (FAST) WH_T(3);
-  store_env<C>(s, L, a.state_out ? a.state_out : a.state, a.B, e, na, tid);
+  store_env<C>(s, L, a.state_out ? a.state_out : a.state, a.B, e0, na, tid);
 #ifdef WH_TIMING
   if (FAST) {
     __builtin_amdgcn_s_waitcnt(0);   // the state stores have left the wave
@@ -1765,7 +1895,7 @@ __global__ __launch_bounds__(BT) void k_reset(ResetParams a) {
     reset_philox<C>(s, L, Keys{a.k0, a.k1}, (uint32_t)(a.env_offset + e), a.na, a.variable_n,
                     (uint32_t)a.W, tid);
   if (!a.injected) WH_CHECK_ENV(s, L, e, tid);   // injected draws may legitimately be partial
-  store_env<C>(s, L, a.state, a.B, e, a.na, tid);
+  store_env<C>(s, L, a.state, a.B, (int64_t)blockIdx.x * BT, a.na, tid);
 }
 
 // Observation rows (core.py:371-432, reset rows core.py:224-260), HBM-write bound.
@@ -2090,12 +2220,21 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   const int na = FAST ? C::NAM : a.na;
   RawEnv<C> raw;
   FastRun<C, POLICY, MULTI> run(a, e);
-  if (loaded) {
-    load_env_issue<C>(raw, a.state, a.B, e, na);
-    if constexpr (FAST) run.load_actions(a, e);
+  uint4 tv0 = make_uint4(0u, 0u, 0u, 0u), tv1 = tv0;
+  if (stepper) {
+    tv0 = issue_table_chunk<C>(a.tables, 0);
+    tv1 = issue_table_chunk<C>(a.tables, 1);
+  }
+  __builtin_amdgcn_sched_barrier(0);   // table loads (L2) ahead of the state planes (HBM), as in k_step
+  // every lane issues the state loads (lanes that own no env re-read env e0's words): under an exec
+  // branch the waitcnt pass would drain them before the table's LDS writes (see k_step)
+  load_env_issue<C>(raw, a.state, a.B, e0, loaded ? tid : 0, na);
+  if constexpr (FAST) {
+    if (loaded) run.load_actions(a, e);
   }
   if (stepper) {
-    load_tables<C>(L.tbl, a.tables);
+    commit_table_chunk<C>(L.tbl, 0, tv0);
+    commit_table_chunk<C>(L.tbl, 1, tv1);
   } else {
     const uint32_t* srcg = &kObsSrcF<C::R, C::NAM>.w[0][0];
     for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
@@ -2125,11 +2264,11 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       if (it > 0) write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
       __syncthreads();
     }
-    if (loaded) store_env<C>(s, L, a.state, a.B, e, na, tid);
+    if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
   } else if constexpr (FAST) {   // one step
     if (loaded) {
       run.step(a, s, L, nullptr, k, gid, e, tid, 0);
-      store_env<C>(s, L, a.state, a.B, e, na, tid);
+      store_env<C>(s, L, a.state, a.B, e0, na, tid);
       write_image<C>(s, L, O, tid, C::NAM, 0);
     }
     __syncthreads();
@@ -2137,7 +2276,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   } else {
     if (stepped) {
       run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
-      store_env<C>(s, L, a.state, a.B, e, na, tid);
+      store_env<C>(s, L, a.state, a.B, e0, na, tid);
     }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
     __syncthreads();
@@ -2275,7 +2414,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   const int D = g.D;
   *bad = 0;
   if (D > 32) { *bad = 1; return {}; }
-  std::vector<uint8_t> cell(256 * D, 0);
+  std::vector<uint8_t> cell(cell_bytes(D), 0);
   std::vector<uint32_t> rp(g.P + 1), tag(g.P + 1);
   rp[g.P] = 0x00FF00FFu;
   tag[g.P] = (63u << 10) | ((uint32_t)(D / 2) << 5) | (uint32_t)(D / 2);   // pickup << 10 | y << 5 | x
@@ -2284,7 +2423,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
       for (int q = 0; q < 4; ++q) {
         const int j = (ix * g.NR + iy) * 4 + q;
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
-        const int ci = x | (y << 8);
+        const int ci = cell_index(x, y);
         if (cell[ci]) *bad = 1;  // overlapping racks
         cell[ci] = (uint8_t)(j + 1);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
@@ -2305,7 +2444,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   std::vector<uint32_t> valid;
   for (int x = 1; x < D - 1; ++x)
     for (int y = 1; y < D - 1; ++y)
-      if (!cell[x | (y << 8)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
+      if (!cell[cell_index(x, y)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
   std::vector<uint32_t> words(cell.size() / 4, 0);
   memcpy(words.data(), cell.data(), cell.size());
   for (int j = 0; j <= g.P; ++j) {

@@ -14,7 +14,8 @@ SPEC.json:
         {"name": "tree"},                             # the production library of this tree
         {"name": "noprog", "flags": "-DWH_X"},        # this tree's sources with -D flags (build_variant.sh)
         {"name": "r04", "rev": "f6d71ed"},            # the library at a git revision (its own Makefile)
-        {"name": "r04x", "rev": "f6d71ed", "flags": "-DWH_Y"}],
+        {"name": "r04x", "rev": "f6d71ed", "flags": "-DWH_Y"},
+        {"name": "l16", "flags": "-DWH_ONLY_LARGE16", "commands": ["..."]}],   # own commands
      "commands": ["python tools/step_probe.py --steps 200 --launches 6",
                   "python tools/step_probe.py --variant large --agents 16 --steps 20 --launches 8"],
      "timeout": 180}
@@ -103,7 +104,7 @@ def run(spec):
     for rnd in range(int(spec.get("rounds", 2))):
         for v in spec["variants"]:
             env = dict(os.environ, WAREHOUSE_AMD_LIB=lib_path(v), WAREHOUSE_AMD_AB="1", **v.get("env", {}))
-            for cmd in spec["commands"]:
+            for cmd in v.get("commands", spec["commands"]):
                 with open(out, "a") as f:
                     f.write(f"lib={v['name']} round={rnd + 1} cmd={cmd}\n")
                     f.flush()

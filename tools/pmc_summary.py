@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_r03.sh (or tools/sq_probe.sh) output directory into profiles/ (committed evidence).
+"""Summarise a tools/profile_round.sh (or tools/sq_probe.sh) output directory into profiles/ (committed evidence).
 
     python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> [--kernel k_step]
 
