@@ -81,10 +81,10 @@ constexpr bool kRegenHoist = false;
 // Regeneration targets of items 1 and 2 by skipping the earlier items' targets (a compare-add each)
 // instead of a rank selection on a used-target mask; the mask is built only from item 3 on.  Same
 // values.  -DWH_NO_REGEN_SKIP: the mask for every item (A/B).
-// -DWH_HOIST_POLICY: the regeneration's first Philox block computed at the top of the fused step,
-// in the policy's basic block (its ten rounds then fill the gaps around the request-table reads)
-// instead of inside the move loop's (A/B).
-#ifdef WH_HOIST_POLICY
+// The regeneration's first Philox block is computed in the fused step's policy block (its ten rounds
+// fill that block's issue gaps) rather than inside the move loop's: -0.5 % per step at Medium-8 and
+// Large-16 (profiles/r05_step3_ab.txt).  -DWH_NO_HOIST_POLICY: inside the move loop (A/B).
+#ifndef WH_NO_HOIST_POLICY
 constexpr bool kHoistPolicy = true;
 #else
 constexpr bool kHoistPolicy = false;
@@ -98,16 +98,21 @@ constexpr bool kRegenSkip = false;
 constexpr uint32_t IDLE = 0xFF00FF00u;    // delivery-target bytes of an idle agent
 constexpr uint32_t XY16 = 0x00FF00FFu;    // position bytes of an agent word
 
-// Cell -> pickup table (u8 per cell).  Default: byte x | y << 8 (one v_perm of the packed position);
-// its dword -- the LDS bank -- is x >> 2, so every lane of a wave reads one of D/4 banks (~8-way
-// conflicts).  -DWH_CELL_SKEW: byte 4x + 132y (one v_dot2 of the masked position), bank (x + y) mod 32.
-#ifdef WH_CELL_SKEW
-constexpr bool kCellSkew = true;
+// Cell -> pickup table (u8 per cell).  Byte x | y << 8 (one v_perm of the packed position): its dword
+// -- the LDS bank -- is x >> 2, so every lane of a wave reads one of D/4 banks (~8- to 13-way
+// conflicts).  Skewed: byte 4x + 132y (one v_dot4_u32_u8 of the agent word), bank (x + y) mod 32.
+// Same-box A/B (profiles/r05_step3_ab.txt): Large-16 -1.6 % per step (-2.9 % with the policy-block
+// Philox hoist), Medium-8 +3 % -- so the skewed table is used from D = 20 (Large) on.
+// -DWH_CELL_SKEW / -DWH_NO_CELL_SKEW force it on / off for every geometry (A/B).
+#if defined(WH_CELL_SKEW)
+__host__ __device__ constexpr bool cell_skew(int) { return true; }
+#elif defined(WH_NO_CELL_SKEW)
+__host__ __device__ constexpr bool cell_skew(int) { return false; }
 #else
-constexpr bool kCellSkew = false;
+__host__ __device__ constexpr bool cell_skew(int D) { return D >= 20; }
 #endif
-__host__ __device__ constexpr int cell_bytes(int D) { return kCellSkew ? 132 * D : 256 * D; }
-__host__ __device__ constexpr int cell_index(int x, int y) { return kCellSkew ? 4 * x + 132 * y : (x | (y << 8)); }
+__host__ __device__ constexpr int cell_bytes(int D) { return cell_skew(D) ? 132 * D : 256 * D; }
+__host__ __device__ constexpr int cell_index(int x, int y, int D) { return cell_skew(D) ? 4 * x + 132 * y : (x | (y << 8)); }
 
 // Shared (per-workgroup) table layout in bytes; built identically by build_tables() on the host.
 struct TableLayout {
@@ -318,9 +323,9 @@ struct Lds {
   // Cell (x | y << 16) -> pickup index + 1, 0 for other cells: one v_perm (the byte index
   // x | y << 8) + one ds_read_u8; the point's row in pkp is then one v_lshl_add away (row_byte).
   __device__ __forceinline__ uint32_t cell_row(uint32_t xy16) const {
-    if constexpr (kCellSkew) {
-      typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-      const uint32_t i = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, xy16 & XY16), (u16x2){4, 132}, 0u, false);
+    if constexpr (cell_skew(C::D)) {
+      // one v_dot4_u32_u8 of the agent word's bytes [x, dx, y, dy] with [4, 0, 132, 0]
+      const uint32_t i = __builtin_amdgcn_udot4(xy16, 0x00840004u, 0u, false);
       return reinterpret_cast<const uint8_t*>(tbl)[i];
     } else {
       return reinterpret_cast<const uint8_t*>(tbl)[__builtin_amdgcn_perm(xy16, xy16, 0x0C0C0200u)];
@@ -2423,7 +2428,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
       for (int q = 0; q < 4; ++q) {
         const int j = (ix * g.NR + iy) * 4 + q;
         const int x = g.racks[ix] - 1 + (q & 1), y = g.racks[iy] - 1 + (q >> 1);
-        const int ci = cell_index(x, y);
+        const int ci = cell_index(x, y, D);
         if (cell[ci]) *bad = 1;  // overlapping racks
         cell[ci] = (uint8_t)(j + 1);
         rp[j] = (uint32_t)x | ((uint32_t)y << 16);
@@ -2444,7 +2449,7 @@ std::vector<uint32_t> build_tables(const Geometry& g, int* bad) {
   std::vector<uint32_t> valid;
   for (int x = 1; x < D - 1; ++x)
     for (int y = 1; y < D - 1; ++y)
-      if (!cell[cell_index(x, y)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
+      if (!cell[cell_index(x, y, D)]) valid.push_back((uint32_t)x | ((uint32_t)y << 16));
   std::vector<uint32_t> words(cell.size() / 4, 0);
   memcpy(words.data(), cell.data(), cell.size());
   for (int j = 0; j <= g.P; ++j) {
@@ -2586,6 +2591,13 @@ bool fused_ok(void (*kern)(StepParams, float*)) {
   seen.emplace_back(reinterpret_cast<const void*>(kern), ok);
   return ok;
 }
+
+// The fused step + rows launch pays while an env's rows are small: at Large-16 (9.3 KB of rows per
+// env, one 512-lane workgroup per CU by LDS) it streams the rows slower than k_observe's small
+// workgroups, 178 vs 137.5 us per sampler step for the two launches; Small-4 13.2 vs 15.1, Medium-8
+// 34.7 vs 40.3 (profiles/r05_step3_ab.txt).  So configurations with more than 4 KB of rows per env
+// take the two launches.
+bool fuse_rows(const Geometry& g) { return 4 * g.NA * (9 * g.R + 1) <= 4096; }
 
 const Kernels* pick(const Geometry& g) {
   const Kernels* best = nullptr;
@@ -2980,7 +2992,7 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
   Geometry g;
   const Kernels* k = nullptr;
   const uint32_t* tab = nullptr;
-  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK) {
+  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && fuse_rows(g)) {
     // the fast instance when the step resolved to it (every env stepped in ascending order, no
     // metrics, auto-reset: RLlib's common case), else the generic one
     void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
@@ -3021,7 +3033,7 @@ int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t po
   Geometry g;
   const Kernels* k = nullptr;
   const uint32_t* tab = nullptr;
-  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && l.kern == k->step_fast[policy] &&
+  if (obs && !unfused && B > 0 && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && fuse_rows(g) && l.kern == k->step_fast[policy] &&
       k->sampler[policy] && fused_ok(k->sampler[policy]) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
     hipLaunchKernelGGL(k->sampler[policy], grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
     return hip_err(hipGetLastError());
@@ -3058,7 +3070,7 @@ int wh_sampler_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t
   if ((rc = prepare(cfg, B, stream, &g, &k, &tab)) != WH_OK) return rc;
   static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
   void (*fk)(StepParams, float*) = steps == 1 ? k->sampler[policy] : k->sampler_multi[policy];
-  if (!unfused && l.kern == k->step_fast[policy] && fk && fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 &&
+  if (!unfused && fuse_rows(g) && l.kern == k->step_fast[policy] && fk && fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 &&
       (uintptr_t)obs % 16 == 0) {
     hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
     return hip_err(hipGetLastError());

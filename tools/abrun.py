@@ -15,7 +15,8 @@ SPEC.json:
         {"name": "noprog", "flags": "-DWH_X"},        # this tree's sources with -D flags (build_variant.sh)
         {"name": "r04", "rev": "f6d71ed"},            # the library at a git revision (its own Makefile)
         {"name": "r04x", "rev": "f6d71ed", "flags": "-DWH_Y"},
-        {"name": "l16", "flags": "-DWH_ONLY_LARGE16", "commands": ["..."]}],   # own commands
+        {"name": "l16", "flags": "-DWH_ONLY_LARGE16", "commands": ["..."]},   # own commands
+        {"name": "tree_x", "lib": "tree", "env": {"WH_SAMPLER_UNFUSED": "1"}}],   # same library, env
      "commands": ["python tools/step_probe.py --steps 200 --launches 6",
                   "python tools/step_probe.py --variant large --agents 16 --steps 20 --launches 8"],
      "timeout": 180}
@@ -39,11 +40,15 @@ PROD = os.path.join(ROOT, "rllib-warehouse_amd", "warehouse", "_lib", "libwareho
 
 
 def lib_path(v):
-    return PROD if v["name"] == "tree" else os.path.join(ROOT, "build_ab", f"{v['name']}.so")
+    """A variant's library; "lib" names another variant's (the same library under other env settings)."""
+    name = v.get("lib", v["name"])
+    return PROD if name == "tree" else os.path.join(ROOT, "build_ab", f"{name}.so")
 
 
 def recipe(v):
     """The command that rebuilds variant v's library from this repository."""
+    if "lib" in v:
+        return f"the library of variant {v['lib']}, run with {v.get('env', {})}"
     if v["name"] == "tree":
         return "make -C rllib-warehouse_amd/csrc (the production library of this tree)"
     if "rev" in v:
@@ -55,6 +60,8 @@ def recipe(v):
 
 def build(spec):
     for v in spec["variants"]:
+        if "lib" in v:
+            continue
         if v["name"] == "tree":
             cmd = ["make", "-s", "-C", CSRC, "-j2"]
             subprocess.run(cmd, check=True)

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--policy", default="greedy")
     ap.add_argument("--train", action="store_true")
     ap.add_argument("--stagger", action="store_true", help="desynchronised episodes (bench.py's desync leg)")
+    ap.add_argument("--cross", action="store_true",
+                    help="place every timed launch across an episode end, as bench.py's window (untimed "
+                         "positioning steps before each launch)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -41,7 +44,14 @@ def main():
     launch = env.rollout_launcher(a.steps, a.policy, 0.0, rewards=rew, dones=dn)
     s = torch.cuda.current_stream(dev)
     times = []
+    T = int(env.geometry["T"])
+    t = 0
     for _ in range(a.launches):
+        if a.cross:   # t + K/2 = T (mod T): the launch's middle step ends the episode
+            pos = (T - a.steps // 2 - t) % T
+            if pos:
+                env.rollout(pos, a.policy, 0.0)
+            t = (t + pos + a.steps) % T
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         launch()
