@@ -62,6 +62,7 @@ constexpr bool kObsNT = true;
 #else
 constexpr bool kObsNT = false;
 #endif
+
 #ifndef WH_REV_SPLIT_MAX_NAM   // agent counts up to which the move loop has the no-reverse-key variant
 #define WH_REV_SPLIT_MAX_NAM 9
 #endif
@@ -531,7 +532,31 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 // Philox blocks, and the whole reset is straight-line code.
 // TO_SLOT: the same draws and results for every lane, written to the lane's reset slot (Lds::rs_*)
 // instead of its registers and pickup plane, for episode epi + 1.
-template <class C, int NAC = -1, bool TO_SLOT = false>
+// The pickup-plane rows (and, with occ, the occupancy rows) of the wave's 64 columns cleared with
+// 16-byte stores, for a reset of every lane of a full wave (synchronised episodes end together): 5
+// stores instead of 36 (Medium) per lane, 4 instead of 16 for the grid.
+template <class C>
+__device__ __forceinline__ void clear_wave_columns(Lds<C>& L, int tid, bool occ) {
+  const int wb = tid & ~63, lane = tid & 63;
+#pragma unroll
+  for (int j0 = 0; j0 < C::P; j0 += 8) {
+    const int j = j0 + (lane >> 3);
+    if (C::P % 8 == 0 || j < C::P)
+      *reinterpret_cast<uint4*>(&L.pkp[j][wb + 8 * (lane & 7)]) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (occ) {
+#pragma unroll
+    for (int y0 = 0; y0 < C::D; y0 += 4) {
+      const int y = y0 + (lane >> 4);
+      if (C::D % 4 == 0 || y < C::D)
+        *reinterpret_cast<uint4*>(&L.occ[y][wb + 4 * (lane & 15)]) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+}
+
+// WAVE: every lane of a full wave resets (the caller checked): the pickup plane is cleared
+// wave-wide with clear_wave_columns.
+template <class C, int NAC = -1, bool TO_SLOT = false, bool WAVE = false>
 __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& k, uint32_t gid,
                                              int na_rt, int variable_n, uint32_t W, int tid,
                                              Slots<C>* RS = nullptr) {
@@ -562,8 +587,12 @@ __device__ __forceinline__ void reset_philox(Regs<C>& s, Lds<C>& L, const Keys& 
     else s.ag[i] = a;
   }
   if (!TO_SLOT) {
+    if constexpr (WAVE) {
+      clear_wave_columns<C>(L, tid, true);
+    } else {
 #pragma unroll
-    for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+      for (int j = 0; j < C::P; ++j) L.pkp[j][tid] = 0;
+    }
   }
   const uint32_t wexp = (W & 0xFFu) << 8;   // opened at t = 0: expires at step W
   uint32_t plo = 0, phi = 0;                // Floyd's subset so far
@@ -1699,6 +1728,10 @@ struct FastRun {
         // short launches (the sampler's 1-step ones): a fill would serve few later resets
         reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
         lg.rebuild = lg.rebuild || done;   // its grid column was cleared
+      } else if (dm == ~0ull) {
+        // every lane of the wave (synchronised episodes): the grid and pickup plane cleared wave-wide
+        reset_philox<C, C::NAM, false, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+        lg.rebuild = true;
       } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
@@ -1776,6 +1809,10 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
         // short launches (the sampler's 1-step ones): a fill would serve few later resets
         reset_lane<C, C::NAM>(s, L, k, gid, a.variable_n, (uint32_t)a.W, tid, __builtin_ctzll(dm));
         lg.rebuild = lg.rebuild || done;   // its grid column was cleared
+      } else if (dm == ~0ull) {
+        // every lane of the wave (synchronised episodes): the grid and pickup plane cleared wave-wide
+        reset_philox<C, C::NAM, false, true>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
+        lg.rebuild = true;
       } else if (done) {
         reset_philox<C, C::NAM>(s, L, k, gid, C::NAM, a.variable_n, (uint32_t)a.W, tid);
 #pragma unroll
@@ -2225,19 +2262,17 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   const int na = FAST ? C::NAM : a.na;
   RawEnv<C> raw;
   FastRun<C, POLICY, MULTI> run(a, e);
-  uint4 tv0 = make_uint4(0u, 0u, 0u, 0u), tv1 = tv0;
+  // The step waves (stepper is wave-uniform: waves 0-3) issue the table loads (L2), then the state
+  // planes (HBM), and write the table to LDS once it has landed, with the state still in flight --
+  // all inside one uniform branch, so the waitcnt pass counts exactly (every step lane loads: a lane
+  // past B re-reads env e0, which exists).  The row waves copy the gather table meanwhile.
   if (stepper) {
-    tv0 = issue_table_chunk<C>(a.tables, 0);
-    tv1 = issue_table_chunk<C>(a.tables, 1);
-  }
-  __builtin_amdgcn_sched_barrier(0);   // table loads (L2) ahead of the state planes (HBM), as in k_step
-  // every lane issues the state loads (lanes that own no env re-read env e0's words): under an exec
-  // branch the waitcnt pass would drain them before the table's LDS writes (see k_step)
-  load_env_issue<C>(raw, a.state, a.B, e0, loaded ? tid : 0, na);
-  if constexpr (FAST) {
-    if (loaded) run.load_actions(a, e);
-  }
-  if (stepper) {
+    const uint4 tv0 = issue_table_chunk<C>(a.tables, 0), tv1 = issue_table_chunk<C>(a.tables, 1);
+    __builtin_amdgcn_sched_barrier(0);   // table loads ahead of the state loads, as in k_step
+    load_env_issue<C>(raw, a.state, a.B, e0, loaded ? tid : 0, na);
+    if constexpr (FAST) {
+      if (loaded) run.load_actions(a, e);
+    }
     commit_table_chunk<C>(L.tbl, 0, tv0);
     commit_table_chunk<C>(L.tbl, 1, tv1);
   } else {
@@ -2261,12 +2296,18 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   if constexpr (FAST && MULTI) {
     if (loaded) RS.rs_ep[tid] = s.epi;   // reset slots start stale (!= epi + 1)
     const int64_t step_floats = a.B * (int64_t)(C::NAM * C::L);
+#ifdef WH_ABLATION
+    const int ablate = a.ablate;   // timing-only: 512 = no steps/images, 256 = no rows
+#else
+    constexpr int ablate = 0;
+#endif
     for (int it = 0; it <= a.steps; ++it) {   // (every wave reaches every barrier)
-      if (loaded && it < a.steps) {
+      if (loaded && it < a.steps && !(ablate & 512)) {
         run.step(a, s, L, &RS, k, gid, e, tid, it);
         write_image<C>(s, L, O, tid, C::NAM, it & 1);
       }
-      if (it > 0) write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+      if (it > 0 && !(ablate & 256))
+        write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
       __syncthreads();
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
