@@ -1969,6 +1969,53 @@ constexpr ObsSrc<R, NAM> make_obs_src() {
 template <int R, int NAM>
 __constant__ ObsSrc<R, NAM> kObsSrc = make_obs_src<R, NAM>();
 
+// The rows [nenv x na x L] f32 of a group's envs from their LDS byte images, float4 q per lane of
+// NT lanes (per env: qe float4s, lim = live floats | fresh << 31, gather bytes from src0 / src1 by
+// freshness).  Every LDS read is unconditional -- a dead value reads a byte of the image (or past the
+// LDS object, which returns 0 without a fault) and is selected away: the conditional form compiled
+// to a branch and an lgkmcnt(0) round trip per float, four serial LDS latencies per store.  Both
+// gather words are read beside lim, so a float4 takes two LDS round trips, and RU float4s per lane
+// are in flight together.
+#ifndef WH_ROWS_RU
+#define WH_ROWS_RU 2
+#endif
+template <int NT, int IMG>
+__device__ __forceinline__ void stream_rows(const uint32_t* lims, const uint32_t* src0, const uint32_t* src1,
+                                            const uint8_t* img, f32x4* __restrict__ out4, uint32_t nenv,
+                                            uint32_t qe, int tid, uint32_t q0 = 0, uint32_t q1 = ~0u) {
+  constexpr int RU = WH_ROWS_RU;
+  const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
+  const uint32_t total = nenv * qe < q1 ? nenv * qe : q1;   // float4s [q0, total) of the group
+  for (uint32_t q = q0 + tid; q < total; q += RU * NT) {
+    f32x4 v[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const uint32_t qu = q + (uint32_t)u * NT < total ? q + (uint32_t)u * NT : q;
+      const uint32_t el4 = __umulhi(qu, magic);
+      const uint32_t k4 = qu - el4 * qe;
+      const uint32_t lim = lims[el4];
+      const uint32_t s0 = src0[k4], s1 = src1[k4];
+      const uint32_t sw = (int32_t)lim < 0 ? s1 : s0;
+      const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
+      const uint8_t* im = img + el4 * IMG;
+      const uint32_t b0 = im[sw & 0xFFu], b1 = im[(sw >> 8) & 0xFFu], b2 = im[(sw >> 16) & 0xFFu],
+                     b3 = im[sw >> 24];
+      v[u].x = lv > 0 ? (float)b0 : 0.0f;
+      v[u].y = lv > 1 ? (float)b1 : 0.0f;
+      v[u].z = lv > 2 ? (float)b2 : 0.0f;
+      v[u].w = lv > 3 ? (float)b3 : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const uint32_t qu = q + (uint32_t)u * NT;
+      if (u == 0 || qu < total) {
+        if constexpr (kObsNT) __builtin_nontemporal_store(v[u], &out4[qu]);
+        else out4[qu] = v[u];
+      }
+    }
+  }
+}
+
 template <class C, int OBS_EB>
 struct ObsLds {
   static constexpr int IMG = (C::L + 3) & ~3;
@@ -2068,20 +2115,25 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
       const uint32_t row = t * 32u + (lane & 31u);   // counted from the group's first env
       const uint32_t el1 = row / (uint32_t)na, i = row - el1 * (uint32_t)na;
       const bool rl = row < rows;
-      const uint32_t lim = rl ? O.lim[el1] : 0u;
+      const uint32_t lim = O.lim[rl ? el1 : 0];
       const bool live_row = rl && i < ((lim & 0x7FFFFFFFu) / L);
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(O.src[lim >> 31]);
       const uint8_t* im = O.img[rl ? el1 : 0];
+      // unconditional gathers (see stream_rows): the index of a padding feature (k >= L) reads a
+      // gather byte past the row, or past the table, and is selected away
+      const uint32_t k0 = 16u * q + 8u * (lane >> 5);
+      uint32_t gb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gb[j] = sb[i * L + k0 + j];
       uint32_t w[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         uint32_t hv[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const uint32_t k = 16u * q + 8u * (lane >> 5) + 2u * jj + u;
-          float v = 0.0f;
-          if (k < (uint32_t)L) v = live_row ? (float)im[sb[i * L + k]] : 0.0f;
-          else if (k < (uint32_t)L + 2u) v = 1.0f;
+          const uint32_t k = k0 + 2u * jj + u;
+          const float x = (float)im[gb[2 * jj + u]];
+          const float v = k < (uint32_t)L ? (live_row ? x : 0.0f) : (k < (uint32_t)L + 2u ? 1.0f : 0.0f);
           hv[u] = __float_as_uint(v) >> 16;   // byte values and 1.0: exact in bf16
         }
         w[jj] = hv[0] | (hv[1] << 16);
@@ -2096,26 +2148,8 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   float* out = obs + e0 * per_env;
   if (quads) {
     // per_env % 4 == 0 and obs 16-byte aligned (checked on the host)
-    const uint32_t qe = per_env >> 2, total = nenv * qe;
-    const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
-    f32x4* out4 = reinterpret_cast<f32x4*>(out);
-    // (unrolling this loop 2x or 4x, reads of a pass issued together, measured no faster: it is
-    // write-bound, tools/obs_bench.py)
-    for (uint32_t q = tid; q < total; q += BT) {
-      const uint32_t el4 = __umulhi(q, magic);
-      const uint32_t k4 = q - el4 * qe;
-      const uint32_t lim = O.lim[el4];
-      const uint32_t sw = O.src[lim >> 31][k4];
-      const int live = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
-      const uint8_t* im = O.img[el4];
-      f32x4 v;
-      v.x = live > 0 ? (float)im[sw & 0xFFu] : 0.0f;
-      v.y = live > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
-      v.z = live > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
-      v.w = live > 3 ? (float)im[sw >> 24] : 0.0f;
-      if constexpr (kObsNT) __builtin_nontemporal_store(v, &out4[q]);
-      else out4[q] = v;
-    }
+    stream_rows<BT, ObsLds<C, OBS_EB>::IMG>(O.lim, O.src[0], O.src[1], &O.img[0][0], reinterpret_cast<f32x4*>(out),
+                                            nenv, per_env >> 2, tid);
   } else {
     const uint32_t total = nenv * per_env;
     const uint32_t magic = 0xFFFFFFFFu / per_env + 1u;
@@ -2215,26 +2249,37 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
 // % 4 == 0 and 16-byte alignment: checked on the host).  (Chunks handed out from an LDS counter, so
 // that the step lanes of a multi-step launch take less once they join late, measured 1.5 us slower
 // on a 1-step launch and no faster on 20- and 100-step ones: profiles/r04_rows_ab.txt.)
+// Every LDS read of a float4 is unconditional (a dead value reads a byte of the image, or past it,
+// which LDS returns as 0 without a fault, and is then selected away): the conditional form compiled
+// to one branch and one lgkmcnt(0) round trip per float, four serial LDS latencies per store.  The
+// gather word of both tables is read beside lim, so a float4 costs two LDS round trips, and RU
+// float4s per lane are in flight together.
 template <class C, int NBUF>
 __device__ __forceinline__ void write_rows(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
                                            uint32_t nenv, uint32_t qe, int tid) {
-  const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
-  const uint32_t total = nenv * qe;
-  f32x4* out4 = reinterpret_cast<f32x4*>(rows);
-  for (uint32_t q = tid; q < total; q += 2 * BT) {
-    const uint32_t el4 = __umulhi(q, magic);
-    const uint32_t k4 = q - el4 * qe;
-    const uint32_t lim = O.lim[buf][el4];
-    const uint32_t sw = O.src[lim >> 31][k4];
-    const int lv = (int)(lim & 0x7FFFFFFFu) - 4 * (int)k4;   // > j  <=>  value j is live
-    const uint8_t* im = O.img[buf][el4];
-    f32x4 v;
-    v.x = lv > 0 ? (float)im[sw & 0xFFu] : 0.0f;
-    v.y = lv > 1 ? (float)im[(sw >> 8) & 0xFFu] : 0.0f;
-    v.z = lv > 2 ? (float)im[(sw >> 16) & 0xFFu] : 0.0f;
-    v.w = lv > 3 ? (float)im[sw >> 24] : 0.0f;
-    out4[q] = v;
+  stream_rows<2 * BT, SampLds<C, NBUF>::IMG>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
+                                             reinterpret_cast<f32x4*>(rows), nenv, qe, tid);
+}
+
+// (A/B, profiles/r05_rowshare_ab.txt) A multi-step launch's rows of step k-1 while the step lanes
+// compute step k: the row lanes take kRowShare % of the float4s, the step lanes the rest.
+#ifndef WH_ROW_SHARE
+#define WH_ROW_SHARE 50
+#endif
+constexpr int kRowShare = WH_ROW_SHARE;
+template <class C, int NBUF>
+__device__ __forceinline__ void write_rows_split(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
+                                                 uint32_t nenv, uint32_t qe, int tid, bool stepped_now) {
+  if (!stepped_now || kRowShare == 50) {
+    write_rows<C>(O, buf, rows, nenv, qe, tid);
+    return;
   }
+  const uint32_t total = nenv * qe;
+  const uint32_t split = (uint32_t)(((uint64_t)total * kRowShare) / 100u);
+  const bool row_lane = tid >= BT;   // wave-uniform
+  stream_rows<BT, SampLds<C, NBUF>::IMG>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
+                                         reinterpret_cast<f32x4*>(rows), nenv, qe, row_lane ? tid - BT : tid,
+                                         row_lane ? 0u : split, row_lane ? split : total);
 }
 
 // FAST: the fused rollout's steps (greedy/random policy, every env stepped, auto-reset): a.steps of
@@ -2307,7 +2352,8 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
         write_image<C>(s, L, O, tid, C::NAM, it & 1);
       }
       if (it > 0 && !(ablate & 256))
-        write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+        write_rows_split<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv,
+                            qe, tid, it < a.steps && !(ablate & 512));
       __syncthreads();
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
