@@ -2261,27 +2261,6 @@ __device__ __forceinline__ void write_rows(const SampLds<C, NBUF>& O, int buf, f
                                              reinterpret_cast<f32x4*>(rows), nenv, qe, tid);
 }
 
-// (A/B, profiles/r05_rowshare_ab.txt) A multi-step launch's rows of step k-1 while the step lanes
-// compute step k: the row lanes take kRowShare % of the float4s, the step lanes the rest.
-#ifndef WH_ROW_SHARE
-#define WH_ROW_SHARE 50
-#endif
-constexpr int kRowShare = WH_ROW_SHARE;
-template <class C, int NBUF>
-__device__ __forceinline__ void write_rows_split(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
-                                                 uint32_t nenv, uint32_t qe, int tid, bool stepped_now) {
-  if (!stepped_now || kRowShare == 50) {
-    write_rows<C>(O, buf, rows, nenv, qe, tid);
-    return;
-  }
-  const uint32_t total = nenv * qe;
-  const uint32_t split = (uint32_t)(((uint64_t)total * kRowShare) / 100u);
-  const bool row_lane = tid >= BT;   // wave-uniform
-  stream_rows<BT, SampLds<C, NBUF>::IMG>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
-                                         reinterpret_cast<f32x4*>(rows), nenv, qe, row_lane ? tid - BT : tid,
-                                         row_lane ? 0u : split, row_lane ? split : total);
-}
-
 // FAST: the fused rollout's steps (greedy/random policy, every env stepped, auto-reset): a.steps of
 // them in one launch (wh_sampler_step: 1; wh_sampler_rollout: a rollout fragment), step k's rows
 // going to obs + k * B * NA * L.  Iteration k of the launch loop: the step lanes compute step k and
@@ -2352,8 +2331,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
         write_image<C>(s, L, O, tid, C::NAM, it & 1);
       }
       if (it > 0 && !(ablate & 256))
-        write_rows_split<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv,
-                            qe, tid, it < a.steps && !(ablate & 512));
+        write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
       __syncthreads();
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
