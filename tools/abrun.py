@@ -53,7 +53,7 @@ def recipe(v):
         return "make -C rllib-warehouse_amd/csrc (the production library of this tree)"
     if "rev" in v:
         return (f"git archive {v['rev']} rllib-warehouse_amd/csrc include | tar -x -C build/rev_{v['name']} && "
-                f"make -C build/rev_{v['name']}/rllib-warehouse_amd/csrc OUT={lib_path(v)} "
+                f"make -C build/rev_{v['name']}/rllib-warehouse_amd/csrc OUT=$PWD/{os.path.relpath(lib_path(v), ROOT)} "
                 + (f"EXTRA='{v['flags']}'" if v.get("flags") else ""))
     return f"bash tools/build_variant.sh {v['name']} {v.get('flags', '')}".strip()
 
