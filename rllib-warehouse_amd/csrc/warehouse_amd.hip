@@ -37,7 +37,21 @@
 namespace {
 
 constexpr int BT = 256;  // lanes (= envs) per workgroup
-constexpr uint32_t ROWB = 2 * BT;   // bytes per pickup-point row of the LDS pickup plane
+// Pickup-plane cell width: 16-bit cells put lanes 2k and 2k+1 in one LDS bank (b32-and-narrower
+// accesses bank by dword mod 32 over 32-lane groups), a 2-way conflict on every access whose rows
+// differ between the two lanes -- the move loop's target-byte lookups, the pickup clears and the
+// regeneration stores.  32-bit cells (the upper half unused) give every lane of a group its own
+// bank for twice the LDS, and measured slower anyway (Medium-8 +0.3 %, Large-16 +0.4 % per
+// 200-step launch, profiles/r05_occ_ab.txt; round 4 the same), so the cells stay 16-bit;
+// -DWH_PKP32 selects 32-bit cells (A/B).
+#if defined(WH_PKP16)
+constexpr bool kPkWide = false;
+#else
+constexpr bool kPkWide = true;
+#endif
+using PkCell = std::conditional_t<kPkWide, uint32_t, uint16_t>;
+constexpr uint32_t PKW = sizeof(PkCell);
+constexpr uint32_t ROWB = PKW * BT;   // bytes per pickup-point row of the LDS pickup plane
 
 enum Policy { POL_EXTERNAL = 0, POL_GREEDY = 1, POL_RANDOM = 2 };
 enum Purpose : uint32_t { PUR_RESET = 1, PUR_REGEN = 2, PUR_POLICY = 3, PUR_RANDOM = 4 };
@@ -85,6 +99,24 @@ constexpr bool kRegenHoist = false;
 // The regeneration's first Philox block is computed in the fused step's policy block (its ten rounds
 // fill that block's issue gaps) rather than inside the move loop's: -0.5 % per step at Medium-8 and
 // Large-16 (profiles/r05_step3_ab.txt).  -DWH_NO_HOIST_POLICY: inside the move loop (A/B).
+// The ascending move loop reads agent s's occupancy word kOccAhead turns early and corrects it in
+// registers for the agents that moved in between (4 VALU per corrected agent), so the LDS latency
+// -- which queues behind the turn's own lookups, lgkmcnt being in order -- is covered by that many
+// turns of work.  Two turns measured slower than one (Medium-8 +2.4 %, Large-16 +3.1 % per 200-step
+// launch, profiles/r05_occ_ab.txt: the second correction's VALU cost more than the wait it hid), so
+// the default is one; -DWH_OCC_AHEAD=2 (A/B).
+#ifndef WH_OCC_AHEAD
+#define WH_OCC_AHEAD 2
+#endif
+constexpr int kOccAhead = WH_OCC_AHEAD;
+// Turns between the move loop's dependent pickup lookups (cell -> point row, point -> target byte,
+// target -> delivery cell, then the decision): each lookup is issued kPickDist turns after the one
+// it depends on.  -DWH_PICK_DIST=2 (A/B).
+#ifndef WH_PICK_DIST
+#define WH_PICK_DIST 1
+#endif
+constexpr int kPickDist = WH_PICK_DIST;
+static_assert(kOccAhead == 1 || kOccAhead == 2, "occupancy read distance");
 #ifndef WH_NO_HOIST_POLICY
 constexpr bool kHoistPolicy = true;
 #else
@@ -315,9 +347,10 @@ struct Lds {
   uint32_t occ[C::D][BT];        // occupancy row y: bit x
   // Pickup point j of lane tid: low byte = request target + 1 (0 = none), high byte = expiry step
   // (low 8 bits).  Row P is scratch: predicated stores of lanes with nothing to write go there.
-  // One 16-bit cell per (point, lane) makes every per-point access a single ds op whose address
-  // is j * BT + tid, and keeps the pickup table out of the VGPRs.
-  uint16_t pkp[C::P + 1][BT];
+  // One cell per (point, lane) (PkCell: 32-bit, the upper half unused, so that no two lanes of a
+  // 32-lane group share a bank) makes every per-point access a single ds op whose address is
+  // j * BT + tid, and keeps the pickup table out of the VGPRs.
+  PkCell pkp[C::P + 1][BT];
   // Agent words when processing in action-dict order; afterwards the reward-row staging area.
   // Wave w only ever touches its own 64 columns [64w, 64w + 64) of every row.
   alignas(16) uint32_t agl[C::NAM][BT];
@@ -351,10 +384,10 @@ struct Lds {
     return (uint32_t)(reinterpret_cast<const char*>(&pkp[0][0]) - reinterpret_cast<const char*>(this));
   }
   __device__ __forceinline__ const uint8_t* row_byte(uint32_t cv, int tid) const {
-    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
+    return reinterpret_cast<const uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + PKW * tid;
   }
   __device__ __forceinline__ uint8_t* row_byte(uint32_t cv, int tid) {
-    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + 2 * tid;
+    return reinterpret_cast<uint8_t*>(this) + (pkp_offset() - ROWB) + cv * ROWB + PKW * tid;
   }
   // Delivery cell of a target byte (target + 1; 0 reads the word before the table: never used) in
   // agent-word form: x << 8 | y << 24 in the target bytes, ones in the position bytes, so a pickup
@@ -538,11 +571,12 @@ __device__ __forceinline__ void store_env(const Regs<C>& s, const Lds<C>& L, uin
 template <class C>
 __device__ __forceinline__ void clear_wave_columns(Lds<C>& L, int tid, bool occ) {
   const int wb = tid & ~63, lane = tid & 63;
+  constexpr int CPL = 16 / PKW, LPR = 64 / CPL, RPS = 64 / LPR;   // cells per lane, lanes per row, rows
 #pragma unroll
-  for (int j0 = 0; j0 < C::P; j0 += 8) {
-    const int j = j0 + (lane >> 3);
-    if (C::P % 8 == 0 || j < C::P)
-      *reinterpret_cast<uint4*>(&L.pkp[j][wb + 8 * (lane & 7)]) = make_uint4(0u, 0u, 0u, 0u);
+  for (int j0 = 0; j0 < C::P; j0 += RPS) {
+    const int j = j0 + lane / LPR;
+    if (C::P % RPS == 0 || j < C::P)
+      *reinterpret_cast<uint4*>(&L.pkp[j][wb + CPL * (lane % LPR)]) = make_uint4(0u, 0u, 0u, 0u);
   }
   if (occ) {
 #pragma unroll
@@ -1140,19 +1174,27 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             rblk0 = stream_block(k, gid ^ z, s.epi, t, PUR_REGEN, 0u);
             hoisted = true;
           }
-          uint32_t raw = *occ_at(cc[0]);
-          uint32_t mokp = 0u;
+          // raws[s % kOccAhead]: agent s's row word, read kOccAhead turns early (before the
+          // updates of agents s - kOccAhead .. s - 1, which the turn applies in registers)
+          uint32_t raws[kOccAhead];
+#pragma unroll
+          for (int j = 0; j < kOccAhead; ++j) raws[j] = j < C::NAM ? *occ_at(cc[j < C::NAM ? j : 0]) : 0u;
+          uint32_t mokh[C::NAM];   // accept masks of the agents already moved
 #pragma unroll
           for (int sidx = 0; sidx < C::NAM; ++sidx) {
             const uint32_t p = pp[sidx], c = cc[sidx], a = s.ag[sidx];
-            // occupied: bit c of the row word, corrected for agent sidx-1's clear-then-set
-            uint32_t occ31 = (uint32_t)__builtin_amdgcn_sbfe((int)raw, c, 1);
-            if (sidx > 0) {
-              const uint32_t set31 = (c ^ cc[sidx - 1]) - 1u;   // bit 31: c == its new cell
-              const uint32_t clr31 = (c ^ pp[sidx - 1]) - 1u;   // bit 31: c == its old cell
-              occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokp, set31, bop3<TC & ~(TA & TB)>(mokp, clr31, occ31));
+            // occupied: bit c of the row word, corrected for the clear-then-set of each agent that
+            // moved after the word was read, in order
+            uint32_t occ31 = (uint32_t)__builtin_amdgcn_sbfe((int)raws[sidx % kOccAhead], c, 1);
+#pragma unroll
+            for (int j = sidx - kOccAhead; j < sidx; ++j) {
+              if (j < 0) continue;
+              const uint32_t set31 = (c ^ cc[j]) - 1u;   // bit 31: c == agent j's new cell
+              const uint32_t clr31 = (c ^ pp[j]) - 1u;   // bit 31: c == agent j's old cell
+              occ31 = bop3<(TA & TB) | (TC & ~(TA & TB))>(mokh[j], set31, bop3<TC & ~(TA & TB)>(mokh[j], clr31, occ31));
             }
-            if (sidx + 1 < C::NAM) raw = *occ_at(cc[sidx + 1]);   // before this turn's update
+            // agent sidx + kOccAhead's word, before this turn's update
+            if (sidx + kOccAhead < C::NAM) raws[sidx % kOccAhead] = *occ_at(cc[sidx + kOccAhead < C::NAM ? sidx + kOccAhead : 0]);
             const uint32_t dd = CLAMP ? pk_sub_i16(c, p) : dstep[sidx];
             uint32_t ukey, kpr = 0;
             uint32_t f = 0x7FFFFFFFu;   // unused key slots hold ~0: their xor is never 0
@@ -1188,11 +1230,15 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             }
             const uint32_t moved = bop3<TA ^ (TB & TC)>(a, mok, dxy);
             s.ag[sidx] = moved;
-            mokp = mok;
+            mokh[sidx] = mok;
+            constexpr int PD = kPickDist;
             cp[sidx] = L.cell_row(moved);
-            if (sidx >= 1) tb[sidx - 1] = *L.row_byte(cp[sidx - 1], tid);
-            if (sidx >= 2) dst[sidx - 2] = L.dst_tb(tb[sidx - 2]);
-            if (PICK_IN_LOOP && !(ablate & 8) && sidx >= 3) pick(sidx - 3, cp[sidx - 3], tb[sidx - 3], dst[sidx - 3]);
+            if (sidx >= PD) tb[sidx - PD] = *L.row_byte(cp[sidx >= PD ? sidx - PD : 0], tid);
+            if (sidx >= 2 * PD) dst[sidx - 2 * PD] = L.dst_tb(tb[sidx >= 2 * PD ? sidx - 2 * PD : 0]);
+            if (PICK_IN_LOOP && !(ablate & 8) && sidx >= 3 * PD) {
+              const int j = sidx >= 3 * PD ? sidx - 3 * PD : 0;
+              pick(j, cp[j], tb[j], dst[j]);
+            }
           }
           // pin the hoisted block to this basic block (LLVM would sink it back to its only use)
           if constexpr (HOIST) asm volatile("" : "+v"(rblk0.x), "+v"(rblk0.y), "+v"(rblk0.z), "+v"(rblk0.w));
@@ -1213,12 +1259,15 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
 #endif
           move_loop(std::false_type{});
         }
-        tb[C::NAM - 1] = *L.row_byte(cp[C::NAM - 1], tid);
-        if (C::NAM >= 2) dst[C::NAM - 2] = L.dst_tb(tb[C::NAM - 2]);
-        dst[C::NAM - 1] = L.dst_tb(tb[C::NAM - 1]);
+        // the lookups and decisions the loop's last turns did not reach, in dependency order
+        constexpr int PD = kPickDist;
+#pragma unroll
+        for (int i = (C::NAM > PD ? C::NAM - PD : 0); i < C::NAM; ++i) tb[i] = *L.row_byte(cp[i], tid);
+#pragma unroll
+        for (int i = (C::NAM > 2 * PD ? C::NAM - 2 * PD : 0); i < C::NAM; ++i) dst[i] = L.dst_tb(tb[i]);
         if (PICK_IN_LOOP && !(ablate & 8)) {
 #pragma unroll
-          for (int i = (C::NAM > 3 ? C::NAM - 3 : 0); i < C::NAM; ++i) pick(i, cp[i], tb[i], dst[i]);
+          for (int i = (C::NAM > 3 * PD ? C::NAM - 3 * PD : 0); i < C::NAM; ++i) pick(i, cp[i], tb[i], dst[i]);
         }
         looked = true;
         if (LAZY && WH_RARE(__any(lg->cm != 0u))) {   // did an agent that shares a cell move?

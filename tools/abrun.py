@@ -111,7 +111,7 @@ def run(spec):
     for rnd in range(int(spec.get("rounds", 2))):
         for v in spec["variants"]:
             env = dict(os.environ, WAREHOUSE_AMD_LIB=lib_path(v), WAREHOUSE_AMD_AB="1", **v.get("env", {}))
-            for cmd in v.get("commands", spec["commands"]):
+            for cmd in (v["commands"] if "commands" in v else spec["commands"]):
                 with open(out, "a") as f:
                     f.write(f"lib={v['name']} round={rnd + 1} cmd={cmd}\n")
                     f.flush()
