@@ -44,10 +44,10 @@ constexpr int BT = 256;  // lanes (= envs) per workgroup
 // bank for twice the LDS, and measured slower anyway (Medium-8 +0.3 %, Large-16 +0.4 % per
 // 200-step launch, profiles/r05_occ_ab.txt; round 4 the same), so the cells stay 16-bit;
 // -DWH_PKP32 selects 32-bit cells (A/B).
-#if defined(WH_PKP16)
-constexpr bool kPkWide = false;
-#else
+#if defined(WH_PKP32)
 constexpr bool kPkWide = true;
+#else
+constexpr bool kPkWide = false;
 #endif
 using PkCell = std::conditional_t<kPkWide, uint32_t, uint16_t>;
 constexpr uint32_t PKW = sizeof(PkCell);
@@ -106,7 +106,7 @@ constexpr bool kRegenHoist = false;
 // launch, profiles/r05_occ_ab.txt: the second correction's VALU cost more than the wait it hid), so
 // the default is one; -DWH_OCC_AHEAD=2 (A/B).
 #ifndef WH_OCC_AHEAD
-#define WH_OCC_AHEAD 2
+#define WH_OCC_AHEAD 1
 #endif
 constexpr int kOccAhead = WH_OCC_AHEAD;
 // Turns between the move loop's dependent pickup lookups (cell -> point row, point -> target byte,
