@@ -17,17 +17,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int OPS = 64;   // staged A operands of 1 KiB (64 KiB of LDS, as one k_mlp16 stage)
 
-template <bool LDS_A>
-__global__ __launch_bounds__(512) void k(float* out, const uint4* __restrict__ src, int iters) {
+// WAVES waves per workgroup (8: two per SIMD, 4: one), NT 16-sample tiles per A operand read
+template <bool LDS_A, int WAVES = 8, int NT = 2>
+__global__ __launch_bounds__(64 * WAVES) void k(float* out, const uint4* __restrict__ src, int iters) {
   __shared__ uint4 lds[OPS * 64];
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < OPS * 64; i += 512) lds[i] = src[i];
+  for (int i = tid; i < OPS * 64; i += 64 * WAVES) lds[i] = src[i];
   __syncthreads();
-  const uint4 r0 = src[(blockIdx.x * 512 + tid) % (OPS * 64)], r1 = src[(blockIdx.x * 512 + tid + 7) % (OPS * 64)];
-  const bf16x8 b0 = __builtin_bit_cast(bf16x8, r0), b1 = __builtin_bit_cast(bf16x8, r1);
+  bf16x8 bt[NT];
+  for (int t = 0; t < NT; ++t) bt[t] = __builtin_bit_cast(bf16x8, src[(blockIdx.x * 512 + tid + 7 * t) % (OPS * 64)]);
   bf16x8 areg[4];
   for (int j = 0; j < 4; ++j) areg[j] = __builtin_bit_cast(bf16x8, src[(tid * 4 + j) % (OPS * 64)]);
-  f32x4 acc[8] = {};
+  f32x4 acc[4 * NT] = {};
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int g = 0; g < OPS; g += 4) {
@@ -36,19 +37,19 @@ __global__ __launch_bounds__(512) void k(float* out, const uint4* __restrict__ s
       for (int j = 0; j < 4; ++j)
         a[j] = LDS_A ? __builtin_bit_cast(bf16x8, lds[(g + j) * 64 + lane]) : areg[j];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b0, acc[2 * j], 0, 0, 0);
-        acc[2 * j + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b1, acc[2 * j + 1], 0, 0, 0);
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[NT * j + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bt[t], acc[NT * j + t], 0, 0, 0);
     }
   }
   float s = 0.0f;
-  for (int t = 0; t < 8; ++t)
+  for (int t = 0; t < 4 * NT; ++t)
     for (int q = 0; q < 4; ++q) s += acc[t][q];
   out[blockIdx.x * 512 + tid] = s;
 }
 
-template <bool LDS_A>
+template <bool LDS_A, int WAVES = 8, int NT = 2>
 void run(const char* name, float* out, const uint4* src, int grid, int iters) {
   // >= 2 s of back-to-back launches first, so the clock has settled (MI355X_MICROARCH.md item 6)
   hipEvent_t a, b;
@@ -58,7 +59,7 @@ void run(const char* name, float* out, const uint4* src, int grid, int iters) {
   int warm = 0;
   float ms = 0.0f;
   do {
-    hipLaunchKernelGGL(k<LDS_A>, dim3(grid), dim3(512), 0, 0, out, src, iters);
+    hipLaunchKernelGGL((k<LDS_A, WAVES, NT>), dim3(grid), dim3(64 * WAVES), 0, 0, out, src, iters);
     ++warm;
     hipEventRecord(b);
     hipEventSynchronize(b);
@@ -66,13 +67,14 @@ void run(const char* name, float* out, const uint4* src, int grid, int iters) {
   } while (ms < 2000.0f);
   const int reps = 20;
   hipEventRecord(a);
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k<LDS_A>, dim3(grid), dim3(512), 0, 0, out, src, iters);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((k<LDS_A, WAVES, NT>), dim3(grid), dim3(64 * WAVES), 0, 0, out, src, iters);
   hipEventRecord(b);
   hipEventSynchronize(b);
   hipEventElapsedTime(&ms, a, b);
-  const double flop = (double)grid * 8 * iters * OPS * 2 * (16.0 * 16 * 32 * 2) * reps;
-  printf("%-34s grid %d x 512: %.3f ms per launch, %.1f TFLOP/s = %.3f of 2.5 PF (after %d warm-up launches)\n", name,
-         grid, ms / reps, flop / (ms * 1e-3) / 1e12, flop / (ms * 1e-3) / 2.5e15, warm);
+  const double flop = (double)grid * WAVES * iters * OPS * NT * (16.0 * 16 * 32 * 2) * reps;
+  printf("%-44s grid %d x %d: %.3f ms per launch, %.1f TFLOP/s = %.3f of 2.5 PF (after %d warm-up launches)\n", name,
+         grid, 64 * WAVES, ms / reps, flop / (ms * 1e-3) / 1e12, flop / (ms * 1e-3) / 2.5e15, warm);
 }
 
 int main() {
@@ -93,8 +95,11 @@ int main() {
   hipMalloc(&out, (size_t)cus * 512 * 4);
   hipMemcpy(src, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   const int iters = 1024;
-  run<true>("16x16x32, A from LDS (k_mlp16 shape)", out, src, cus, iters);
-  run<false>("16x16x32, operands in registers", out, src, cus, iters);
+  run<true, 8, 2>("A from LDS, 2 waves/SIMD, 2 tiles (k_mlp16)", out, src, cus, iters);
+  run<false, 8, 2>("registers, 2 waves/SIMD, 2 tiles", out, src, cus, iters);
+  run<true, 4, 4>("A from LDS, 1 wave/SIMD, 4 tiles", out, src, cus, iters / 2);
+  run<true, 4, 2>("A from LDS, 1 wave/SIMD, 2 tiles", out, src, cus, iters);
+  run<true, 8, 4>("A from LDS, 2 waves/SIMD, 4 tiles", out, src, cus, iters / 2);
   hipFree(src);
   hipFree(out);
   return 0;
