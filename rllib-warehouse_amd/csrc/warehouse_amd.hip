@@ -111,9 +111,11 @@ constexpr bool kRegenHoist = false;
 constexpr int kOccAhead = WH_OCC_AHEAD;
 // Turns between the move loop's dependent pickup lookups (cell -> point row, point -> target byte,
 // target -> delivery cell, then the decision): each lookup is issued kPickDist turns after the one
-// it depends on.  -DWH_PICK_DIST=2 (A/B).
+// it depends on, so its LDS latency is covered by that many turns of the serial chain.  Two turns:
+// Medium-8 -1.0 %, Large-16 -1.0 % per 200-step launch against one (profiles/r05_pick_ab.txt);
+// -DWH_PICK_DIST=1 / 3 (A/B).
 #ifndef WH_PICK_DIST
-#define WH_PICK_DIST 1
+#define WH_PICK_DIST 2
 #endif
 constexpr int kPickDist = WH_PICK_DIST;
 static_assert(kOccAhead == 1 || kOccAhead == 2, "occupancy read distance");
