@@ -169,8 +169,11 @@ __device__ __forceinline__ void stage_chunk(const u32x4* __restrict__ src, u32x4
 // NOPS consecutive staged operands, each fed to MFMA f(i, A fragment): fragments are read from LDS
 // DEPTH groups of GS ahead of their MFMAs; the sched_barriers keep the reads ahead of the MFMAs and
 // stop the compiler from hoisting a whole chunk's reads (NOPS x 4 VGPRs would spill).
-template <int NOPS, int GS_ = 4, int DEPTH = 2, class F>
-__device__ __forceinline__ void stream_ops(const u32x4* S, int lane, F&& f) {
+struct NoPre {
+  __device__ __forceinline__ void operator()(int, int) const {}
+};
+template <int NOPS, int GS_ = 4, int DEPTH = 2, class F, class P = NoPre>
+__device__ __forceinline__ void stream_ops(const u32x4* S, int lane, F&& f, P&& pre = P{}) {
   constexpr int GS = NOPS % GS_ == 0 ? GS_ : 2, NG = NOPS / GS;
   static_assert(NOPS % GS == 0 && NG >= DEPTH, "operand groups");
   bf16x8 buf[DEPTH + 1][GS];
@@ -184,6 +187,7 @@ __device__ __forceinline__ void stream_ops(const u32x4* S, int lane, F&& f) {
 #pragma unroll
       for (int i = 0; i < GS; ++i) buf[(gi + DEPTH) % (DEPTH + 1)][i] = frag(S + ((gi + DEPTH) * GS + i) * 64 + lane);
     }
+    pre(gi, NG);                                   // (k_mlp16: this group's share of the next chunk's DMA)
     __builtin_amdgcn_sched_barrier(0);             // later groups' reads issue BEFORE this group's MFMAs
 #pragma unroll
     for (int i = 0; i < GS; ++i) f(gi * GS + i, buf[gi % (DEPTH + 1)][i]);
@@ -462,14 +466,20 @@ __global__ __launch_bounds__(N::MT) void k_mlp(MlpArgs a) {
 //  MODE 0: layer 0 group by group (all H0 units kept as B fragments, 2 x 4 VGPRs per group), then
 //    layer 1 group by group with K = H0 at hand, each group's two tiles feeding one W2 k-step.
 //  MODE 1 (Large): all layer-1 tiles live (2 x 4 VGPRs each); layer-0 groups streamed through them.
-template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_>
+//  NS (2 or 4): 16-sample tiles per wave, each staged A fragment feeding NS MFMAs.  NS = 2 at 8 waves
+//    (two per SIMD, 256 registers each); NS = 4 at 4 waves (one per SIMD, 512 registers): the same
+//    256 samples per task, half the fragment reads per MFMA, and the bare loop of that shape holds
+//    1,998 against 1,472 TFLOP/s on random data (tools/mfma16_ceiling.hip, profiles/r05_mfma16_ceiling.txt).
+template <int IN_, int H0_, int H1_, int WAVES_, int MODE_, int L0T_, int L1T_, int NS_ = 2>
 struct Net16 {
   static constexpr int IN = IN_, INP = (IN_ + 2 + 31) / 32 * 32, H0 = H0_, H1 = H1_, OUT = 9;
+  static constexpr int NS = NS_;
   static constexpr int KQ0 = INP / 32;              // layer-0 k-steps of 32
   static constexpr int KQX = (IN_ + 2 + 15) / 16;   // k-steps of 16 in wh_observe_x's operand
   static constexpr int G0 = H0 / 32, G1 = H1 / 32;  // groups of 32 hidden units
-  static constexpr int WAVES = WAVES_, MT = 64 * WAVES_, ROWS = 32 * WAVES_;
+  static constexpr int WAVES = WAVES_, MT = 64 * WAVES_, ROWS = 16 * NS_ * WAVES_;
   static constexpr int MODE = MODE_, L0T = L0T_, L1T = L1T_;
+  static_assert(NS_ == 2 || NS_ == 4, "16-sample tiles per wave: two per 32-row operand tile");
   static constexpr int U0 = MODE == 0 ? 2 * KQ0 : 2 * KQ0 + 2 * G1;   // operands per layer-0 group
   static constexpr int U1 = 2 * G0 + 1;                               // MODE 0: per layer-1 group (+ W2)
   static constexpr int L0C = G0 / L0T, L0OPS = L0T * U0;
@@ -505,13 +515,14 @@ __device__ __forceinline__ bf16x8 group_frag_bias(f32x4 t0, f32x4 t1, const floa
 }
 
 // Logits of sample tile s: output o of sample n sits in lane n + 16 (o >> 2), register o & 3.  Lanes
-// 16s .. 16s + 15 gather their sample's nine and emit it (32 samples per wave).
-__device__ __forceinline__ void emit_logits16(const f32x4 (&lg)[2], const float* b2, int64_t row0, int64_t rows,
+// 16s .. 16s + 15 gather their sample's nine and emit it (16 NS samples per wave).
+template <int NS>
+__device__ __forceinline__ void emit_logits16(const f32x4 (&lg)[NS], const float* b2, int64_t row0, int64_t rows,
                                               int lane, const MlpArgs& a) {
   const int n = lane & 15, part = lane >> 4;
   f32x16 z16{};
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
     float v[9];
 #pragma unroll
     for (int o = 0; o < 9; ++o) v[o] = __shfl(lg[s][o & 3], n + 16 * (o >> 2));
@@ -521,7 +532,7 @@ __device__ __forceinline__ void emit_logits16(const f32x4 (&lg)[2], const float*
     }
   }
   const int64_t row = row0 + 16 * part + n;
-  if (part < 2 && row < rows) {
+  if (part < NS && row < rows) {
     constexpr int OUT = 9;
     float z[OUT];
 #pragma unroll
@@ -560,6 +571,39 @@ __device__ __forceinline__ void emit_logits16(const f32x4 (&lg)[2], const float*
   }
 }
 
+// The next chunk's LDS-DMA pieces, spread over the current chunk's operand groups (group gi of NG
+// issues this wave's pieces j in [gi NPW / NG, (gi + 1) NPW / NG)) instead of all at the chunk's
+// start, where each piece's issue competes with the chunk's first fragment reads (100-185 cycles a
+// piece there against ~60 among MFMAs, MI355X_MICROARCH.md).  -DWH_MLP_NO_SPREAD: at the start (A/B).
+#ifndef WH_MLP_NO_SPREAD
+constexpr bool kSpreadDma = true;
+#else
+constexpr bool kSpreadDma = false;
+#endif
+struct NextChunk {
+  const u32x4* src;
+  int dst;    // LDS stage, in 16-byte units from the kernel's LDS object
+  int nops;   // 0: no next chunk
+};
+template <class N>
+__device__ __forceinline__ void stage_slice(u32x4* lds, const NextChunk& nc, int gi, int ng, int w, int lane) {
+  constexpr int NPW = (N::SOPS + N::WAVES - 1) / N::WAVES;   // pieces per wave, at most
+  const int j0 = (gi * NPW + ng - 1) / ng, j1 = ((gi + 1) * NPW + ng - 1) / ng;
+  for (int j = j0; j < j1; ++j) {
+    const int o = w + N::WAVES * j;   // wave-uniform: SGPR bases, one lane offset VGPR
+    if (o < nc.nops) __builtin_amdgcn_global_load_lds(nc.src + o * 64 + lane, lds + nc.dst + o * 64, 16, 0, 0);
+  }
+}
+// (the LDS destination stays an offset from the __shared__ object: a generic pointer rebuilt from
+// its low 32 bits is NULL for offset 0, and its cast to the LDS address space then yields the LDS
+// null value, not offset 0)
+__device__ __forceinline__ NextChunk uniform_chunk(const u32x4* src, int dst, int nops) {
+  const uint64_t sa = reinterpret_cast<uint64_t>(src);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sa), hi = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32));
+  return NextChunk{reinterpret_cast<const u32x4*>(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(dst),
+                   __builtin_amdgcn_readfirstlane(nops)};
+}
+
 template <class N>
 __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
   // ONE __shared__ object (see k_mlp)
@@ -582,31 +626,39 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
       stage_chunk<N>(chunks + N::chunk_off(c) * 64, stage_of(gg), N::chunk_ops(c), w, lane);
     }
   };
+  auto next_of = [&](int gg) -> NextChunk {
+    if (gg >= my_tasks * N::NCH) return NextChunk{chunks, 0, 0};
+    const int c = gg % N::NCH;
+    return uniform_chunk(chunks + N::chunk_off(c) * 64, (gg & 1) * (N::SOPS * 64), N::chunk_ops(c));
+  };
   fetch(0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
 
   // X^T fragments xb[q][s]: lane (n, g) holds features 32q + 8g + j of sample 16s + n of the wave
-  bf16x8 xb[N::KQ0][2];
+  constexpr int NS = N::NS;
+  bf16x8 xb[N::KQ0][NS];
   const bool xf = a.xfrag != nullptr;
   auto load_x = [&](int64_t task_i) {
-    const int64_t r0 = task_i * N::ROWS + w * 32;
+    const int64_t r0 = task_i * N::ROWS + w * (16 * NS);
     if (xf) {
       // wh_observe_x's 32x32x16 fragment order: 16-byte chunk ((tile * KQX + q16) * 64 + h * 32 + r)
-      // holds features 16 q16 + 8 h + j of row r of the 32-row tile
-      int64_t tile = task_i * N::WAVES + w;
-      tile = tile * 32 < a.rows ? tile : 0;
-      const u32x4* src = a.xfrag + tile * (N::KQX * 64);
+      // holds features 16 q16 + 8 h + j of row r of the 32-row tile; sample tile s of the wave is
+      // rows 16 (s & 1) .. + 15 of the wave's 32-row tile s >> 1
 #pragma unroll
-      for (int q = 0; q < N::KQ0; ++q)
+      for (int s = 0; s < NS; ++s) {
+        int64_t tile = (task_i * N::WAVES + w) * (NS / 2) + (s >> 1);
+        tile = tile * 32 < a.rows ? tile : 0;
+        const u32x4* src = a.xfrag + tile * (N::KQX * 64);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int q = 0; q < N::KQ0; ++q) {
           const int q16 = 2 * q + (g >> 1);
-          xb[q][s] = q16 < N::KQX ? frag(src + q16 * 64 + (g & 1) * 32 + 16 * s + n) : bf16x8{};
+          xb[q][s] = q16 < N::KQX ? frag(src + q16 * 64 + (g & 1) * 32 + 16 * (s & 1) + n) : bf16x8{};
         }
+      }
     } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NS; ++s) {
         const int64_t row = r0 + 16 * s + n;
         const bool lv = row < a.rows;
         const float* x = a.obs + (lv ? row : 0) * N::IN;
@@ -630,21 +682,23 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
     const int64_t task = blockIdx.x + (int64_t)it * gridDim.x;
     const int base = it * N::NCH;
     const bool has_next = it + 1 < my_tasks;
-    f32x4 lg[2] = {f32x4{}, f32x4{}};
+    f32x4 lg[NS];
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) lg[s2] = f32x4{};
     if constexpr (N::MODE == 0) {
-      bf16x8 hb[N::G0][2];
+      bf16x8 hb[N::G0][NS];
 #pragma unroll
       for (int c = 0; c < N::L0C; ++c) {
         const int gg = base + c;
-        fetch(gg + 1);
-        f32x4 acc[2][2];
+        fetch(gg + 1);   // (spread over the group stream it cost registers: layer 0's fragments are all live)
+        f32x4 acc[2][NS];
         stream_ops<N::L0OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int m = i / N::U0, k = i % N::U0, rt = k / N::KQ0, q = k % N::KQ0;
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc[rt][s2]);
+          for (int s2 = 0; s2 < NS; ++s2) acc[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc[rt][s2]);
           if (k == N::U0 - 1) {
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) hb[c * N::L0T + m][s2] = group_frag(acc[0][s2], acc[1][s2]);
+            for (int s2 = 0; s2 < NS; ++s2) hb[c * N::L0T + m][s2] = group_frag(acc[0][s2], acc[1][s2]);
           }
         });
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -652,69 +706,74 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
       }
       for (int d = 0; d < N::L1C; ++d) {
         const int gg = base + N::L0C + d;
-        fetch(gg + 1);
+        if (!kSpreadDma) fetch(gg + 1);
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
         // the next task's X during the last chunk (X is dead once layer 0 is done; loading it for
         // the whole of layer 1 would keep its registers live beside all of layer 0's fragments)
         if (d == N::L1C - 1 && has_next) load_x(task + gridDim.x);
-        f32x4 acc[2][2];
+        f32x4 acc[2][NS];
         stream_ops<N::L1OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int uu = i / N::U1, k = i % N::U1;
           if (k < 2 * N::G0) {
             const int rt = k / N::G0, m = k % N::G0;
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) acc[rt][s2] = mfma16(af, hb[m][s2], m == 0 ? f32x4{} : acc[rt][s2]);
+            for (int s2 = 0; s2 < NS; ++s2) acc[rt][s2] = mfma16(af, hb[m][s2], m == 0 ? f32x4{} : acc[rt][s2]);
           } else {
             const int u = d * N::L1T + uu;
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
+            for (int s2 = 0; s2 < NS; ++s2)
               lg[s2] = mfma16(af, group_frag_bias(acc[0][s2], acc[1][s2], b1s, 32 * u, g), lg[s2]);
           }
-        });
+        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
     } else {
-      f32x4 acc1[2 * N::G1][2];
+      f32x4 acc1[2 * N::G1][NS];
 #pragma unroll
-      for (int v = 0; v < 2 * N::G1; ++v) acc1[v][0] = acc1[v][1] = f32x4{};
+      for (int v = 0; v < 2 * N::G1; ++v)
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) acc1[v][s2] = f32x4{};
       for (int c = 0; c < N::L0C; ++c) {
         const int gg = base + c;
-        fetch(gg + 1);
-        f32x4 acc0[2][2];
-        bf16x8 hb0[2];
+        if (!kSpreadDma) fetch(gg + 1);
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
+        f32x4 acc0[2][NS];
+        bf16x8 hb0[NS];
         stream_ops<N::L0OPS, 4, 1>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int k = i % N::U0;
           if (k < 2 * N::KQ0) {
             const int rt = k / N::KQ0, q = k % N::KQ0;
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) acc0[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc0[rt][s2]);
+            for (int s2 = 0; s2 < NS; ++s2) acc0[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc0[rt][s2]);
             if (k == 2 * N::KQ0 - 1) {
 #pragma unroll
-              for (int s2 = 0; s2 < 2; ++s2) hb0[s2] = group_frag(acc0[0][s2], acc0[1][s2]);
+              for (int s2 = 0; s2 < NS; ++s2) hb0[s2] = group_frag(acc0[0][s2], acc0[1][s2]);
             }
           } else {
             const int v = k - 2 * N::KQ0;
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) acc1[v][s2] = mfma16(af, hb0[s2], acc1[v][s2]);
+            for (int s2 = 0; s2 < NS; ++s2) acc1[v][s2] = mfma16(af, hb0[s2], acc1[v][s2]);
           }
-        });
+        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
       {
         const int gg = base + N::L0C;
-        fetch(gg + 1);
+        if (!kSpreadDma) fetch(gg + 1);
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
         if (has_next) load_x(task + gridDim.x);
         stream_ops<N::L1OPS, 4, 1>(stage_of(gg), lane, [&](int u, bf16x8 af) {
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
+          for (int s2 = 0; s2 < NS; ++s2)
             lg[s2] = mfma16(af, group_frag_bias(acc1[2 * u][s2], acc1[2 * u + 1][s2], b1s, 32 * u, g), lg[s2]);
-        });
+        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
     }
-    emit_logits16(lg, b2, task * N::ROWS + w * 32, a.rows, lane, a);
+    emit_logits16<NS>(lg, b2, task * N::ROWS + w * (16 * NS), a.rows, lane, a);
   }
 }
 
@@ -996,9 +1055,9 @@ MlpKernel make_mlp() {
   return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp<N>, pack<N>};
 }
 
-template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T>
+template <int IN, int H0, int H1, int WAVES, int MODE, int L0T, int L1T, int NS = 2>
 MlpKernel make_mlp16() {
-  using N = Net16<IN, H0, H1, WAVES, MODE, L0T, L1T>;
+  using N = Net16<IN, H0, H1, WAVES, MODE, L0T, L1T, NS>;
   return MlpKernel{IN, H0, H1, WH_MLP_BF16, N::MT, N::ROWS, N::BYTES, k_mlp16<N>, pack16<N>};
 }
 
@@ -1015,13 +1074,20 @@ const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // (16x16x32 without it: -3 to -8 %, profiles/r04_mlp16_ab.txt).  WH_MLP_LEGACY=1 selects the
   // 32x32x16 kernel everywhere (A/B runs; a blob is packed for the kernel of its process).
   static const bool legacy = getenv("WH_MLP_LEGACY") != nullptr;
+  static const bool w4 = getenv("WH_MLP16_W4") != nullptr;   // (A/B) one wave per SIMD, four sample tiles
   static const MlpKernel reg16[] = {
       make_mlp16<82, 512, 512, 8, 0, 8, 2>(),      // Medium
       make_mlp16<145, 1024, 256, 8, 1, 2, 1>(),    // Large
   };
+  static const MlpKernel reg16w4[] = {
+      make_mlp16<82, 512, 512, 4, 0, 8, 2, 2>(),
+      make_mlp16<145, 1024, 256, 4, 1, 2, 1, 2>(),
+  };
   if (d && d->out_dim == 9 && d->precision == WH_MLP_BF16 && !legacy)
-    for (const auto& k : reg16)
+    for (int i = 0; i < 2; ++i) {
+      const MlpKernel& k = w4 ? reg16w4[i] : reg16[i];
       if (k.in == d->in_dim && k.h0 == d->hidden0 && k.h1 == d->hidden1) return &k;
+    }
   static const MlpKernel reg[] = {
       // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk,
       // next-task X prefetch): 8 waves = two per SIMD (256 registers each)
