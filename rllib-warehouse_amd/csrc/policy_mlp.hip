@@ -1074,20 +1074,16 @@ const MlpKernel* find_mlp(const wh_mlp_desc* d) {
   // (16x16x32 without it: -3 to -8 %, profiles/r04_mlp16_ab.txt).  WH_MLP_LEGACY=1 selects the
   // 32x32x16 kernel everywhere (A/B runs; a blob is packed for the kernel of its process).
   static const bool legacy = getenv("WH_MLP_LEGACY") != nullptr;
-  static const bool w4 = getenv("WH_MLP16_W4") != nullptr;   // (A/B) one wave per SIMD, four sample tiles
+  // (One wave per SIMD -- 4 waves, 128 samples per task, 512 registers -- ran 25-28 % slower: the
+  // weight stream per sample doubles, profiles/r05_mlpw4_ab.txt; four sample tiles per wave to keep
+  // 256 samples per task do not fit 512 registers at Medium.)
   static const MlpKernel reg16[] = {
       make_mlp16<82, 512, 512, 8, 0, 8, 2>(),      // Medium
       make_mlp16<145, 1024, 256, 8, 1, 2, 1>(),    // Large
   };
-  static const MlpKernel reg16w4[] = {
-      make_mlp16<82, 512, 512, 4, 0, 8, 2, 2>(),
-      make_mlp16<145, 1024, 256, 4, 1, 2, 1, 2>(),
-  };
   if (d && d->out_dim == 9 && d->precision == WH_MLP_BF16 && !legacy)
-    for (int i = 0; i < 2; ++i) {
-      const MlpKernel& k = w4 ? reg16w4[i] : reg16[i];
+    for (const auto& k : reg16)
       if (k.in == d->in_dim && k.h0 == d->hidden0 && k.h1 == d->hidden1) return &k;
-    }
   static const MlpKernel reg[] = {
       // (waves per workgroup, dataflow MODE, layer-0 tiles per chunk, layer-1 tiles per chunk,
       // next-task X prefetch): 8 waves = two per SIMD (256 registers each)
