@@ -580,6 +580,11 @@ constexpr bool kSpreadDma = true;
 #else
 constexpr bool kSpreadDma = false;
 #endif
+#ifdef WH_MLP_SPREAD_L0   // (A/B) also in MODE 0's layer-0 chunks
+constexpr bool kSpreadL0 = kSpreadDma;
+#else
+constexpr bool kSpreadL0 = false;
+#endif
 struct NextChunk {
   const u32x4* src;
   int dst;    // LDS stage, in 16-byte units from the kernel's LDS object
@@ -690,7 +695,8 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
 #pragma unroll
       for (int c = 0; c < N::L0C; ++c) {
         const int gg = base + c;
-        fetch(gg + 1);   // (spread over the group stream it cost registers: layer 0's fragments are all live)
+        if (!kSpreadL0) fetch(gg + 1);   // (spread: 46 more registers spilled -- layer 0's fragments are all live)
+        const NextChunk nc = kSpreadL0 ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
         f32x4 acc[2][NS];
         stream_ops<N::L0OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int m = i / N::U0, k = i % N::U0, rt = k / N::KQ0, q = k % N::KQ0;
@@ -700,7 +706,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2) hb[c * N::L0T + m][s2] = group_frag(acc[0][s2], acc[1][s2]);
           }
-        });
+        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
