@@ -580,7 +580,7 @@ constexpr bool kSpreadDma = true;
 #else
 constexpr bool kSpreadDma = false;
 #endif
-#ifdef WH_MLP_SPREAD_L0   // (A/B) also in MODE 0's layer-0 chunks
+#ifdef WH_MLP_SPREAD_L0   // (A/B) also in MODE 0's layer-0 chunks: Medium +13 % (spills), profiles/r05_tune_ab.txt
 constexpr bool kSpreadL0 = kSpreadDma;
 #else
 constexpr bool kSpreadL0 = false;

@@ -112,8 +112,8 @@ constexpr int kOccAhead = WH_OCC_AHEAD;
 // Turns between the move loop's dependent pickup lookups (cell -> point row, point -> target byte,
 // target -> delivery cell, then the decision): each lookup is issued kPickDist turns after the one
 // it depends on, so its LDS latency is covered by that many turns of the serial chain.  Two turns:
-// Medium-8 -1.0 %, Large-16 -1.0 % per 200-step launch against one (profiles/r05_pick_ab.txt);
-// -DWH_PICK_DIST=1 / 3 (A/B).
+// Medium-8 -1.0 %, Large-16 -1.0 % per 200-step launch against one (profiles/r05_pick_ab.txt); three
+// turns +1.3 % / +0.9 % against two (profiles/r05_tune_ab.txt).  -DWH_PICK_DIST=1 / 3 (A/B).
 #ifndef WH_PICK_DIST
 #define WH_PICK_DIST 2
 #endif
