@@ -590,9 +590,17 @@ struct NextChunk {
   int dst;    // LDS stage, in 16-byte units from the kernel's LDS object
   int nops;   // 0: no next chunk
 };
+// The last kSpreadTail % of a chunk's groups issue no pieces, so the last ones have landed when the
+// chunk ends (its vmcnt(0) before the barrier).
+#ifndef WH_MLP_SPREAD_TAIL
+#define WH_MLP_SPREAD_TAIL 0
+#endif
+constexpr int kSpreadTail = WH_MLP_SPREAD_TAIL;
 template <class N>
-__device__ __forceinline__ void stage_slice(u32x4* lds, const NextChunk& nc, int gi, int ng, int w, int lane) {
+__device__ __forceinline__ void stage_slice(u32x4* lds, const NextChunk& nc, int gi, int ng_all, int w, int lane) {
   constexpr int NPW = (N::SOPS + N::WAVES - 1) / N::WAVES;   // pieces per wave, at most
+  const int ng = ng_all - ng_all * kSpreadTail / 100 > 0 ? ng_all - ng_all * kSpreadTail / 100 : 1;
+  if (gi >= ng) return;
   const int j0 = (gi * NPW + ng - 1) / ng, j1 = ((gi + 1) * NPW + ng - 1) / ng;
   for (int j = j0; j < j1; ++j) {
     const int o = w + N::WAVES * j;   // wave-uniform: SGPR bases, one lane offset VGPR

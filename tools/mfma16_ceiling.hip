@@ -49,6 +49,75 @@ __global__ __launch_bounds__(64 * WAVES) void k(float* out, const uint4* __restr
   out[blockIdx.x * 512 + tid] = s;
 }
 
+// k_mlp16's own operand pipeline: stream_ops (fragments read DEPTH = 2 groups of 4 ahead of their
+// MFMAs, sched_barriers around each group), PRIO: s_setprio 1 over each group's MFMAs
+template <int WAVES, bool PRIO>
+__global__ __launch_bounds__(64 * WAVES) void kp(float* out, const uint4* __restrict__ src, int iters) {
+  __shared__ uint4 lds[OPS * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < OPS * 64; i += 64 * WAVES) lds[i] = src[i];
+  __syncthreads();
+  const bf16x8 b0 = __builtin_bit_cast(bf16x8, src[(blockIdx.x * 512 + tid) % (OPS * 64)]);
+  const bf16x8 b1 = __builtin_bit_cast(bf16x8, src[(blockIdx.x * 512 + tid + 7) % (OPS * 64)]);
+  f32x4 acc[8] = {};
+  constexpr int GS = 4, NG = OPS / GS, DEPTH = 2;
+  for (int it = 0; it < iters; ++it) {
+    bf16x8 buf[DEPTH + 1][GS];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int i = 0; i < GS; ++i) buf[d][i] = __builtin_bit_cast(bf16x8, lds[(d * GS + i) * 64 + lane]);
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      if (gi + DEPTH < NG) {
+#pragma unroll
+        for (int i = 0; i < GS; ++i)
+          buf[(gi + DEPTH) % (DEPTH + 1)][i] = __builtin_bit_cast(bf16x8, lds[((gi + DEPTH) * GS + i) * 64 + lane]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < GS; ++i) {
+        acc[2 * i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(buf[gi % (DEPTH + 1)][i], b0, acc[2 * i], 0, 0, 0);
+        acc[2 * i + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(buf[gi % (DEPTH + 1)][i], b1, acc[2 * i + 1], 0, 0, 0);
+      }
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float s = 0.0f;
+  for (int t = 0; t < 8; ++t)
+    for (int q = 0; q < 4; ++q) s += acc[t][q];
+  out[blockIdx.x * 512 + tid] = s;
+}
+
+template <int WAVES, bool PRIO>
+void runp(const char* name, float* out, const uint4* src, int grid, int iters) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  int warm = 0;
+  float ms = 0.0f;
+  do {
+    hipLaunchKernelGGL((kp<WAVES, PRIO>), dim3(grid), dim3(64 * WAVES), 0, 0, out, src, iters);
+    ++warm;
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&ms, a, b);
+  } while (ms < 2000.0f);
+  const int reps = 20;
+  hipEventRecord(a);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((kp<WAVES, PRIO>), dim3(grid), dim3(64 * WAVES), 0, 0, out, src, iters);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  hipEventElapsedTime(&ms, a, b);
+  const double flop = (double)grid * WAVES * iters * OPS * 2 * (16.0 * 16 * 32 * 2) * reps;
+  printf("%-44s grid %d x %d: %.3f ms per launch, %.1f TFLOP/s = %.3f of 2.5 PF (after %d warm-up launches)\n", name,
+         grid, 64 * WAVES, ms / reps, flop / (ms * 1e-3) / 1e12, flop / (ms * 1e-3) / 2.5e15, warm);
+}
+
 template <bool LDS_A, int WAVES = 8, int NT = 2>
 void run(const char* name, float* out, const uint4* src, int grid, int iters) {
   // >= 2 s of back-to-back launches first, so the clock has settled (MI355X_MICROARCH.md item 6)
@@ -100,6 +169,9 @@ int main() {
   run<true, 4, 4>("A from LDS, 1 wave/SIMD, 4 tiles", out, src, cus, iters / 2);
   run<true, 4, 2>("A from LDS, 1 wave/SIMD, 2 tiles", out, src, cus, iters);
   run<true, 8, 4>("A from LDS, 2 waves/SIMD, 4 tiles", out, src, cus, iters / 2);
+  runp<8, false>("stream_ops pipeline, 2 waves/SIMD", out, src, cus, iters);
+  runp<8, true>("stream_ops pipeline + setprio, 2 waves/SIMD", out, src, cus, iters);
+  runp<4, false>("stream_ops pipeline, 1 wave/SIMD", out, src, cus, iters);
   hipFree(src);
   hipFree(out);
   return 0;
