@@ -591,9 +591,10 @@ struct NextChunk {
   int nops;   // 0: no next chunk
 };
 // The last kSpreadTail % of a chunk's groups issue no pieces, so the last ones have landed when the
-// chunk ends (its vmcnt(0) before the barrier).
+// chunk ends (its vmcnt(0) before the barrier): 25 % -2.6 % (Medium) / -1.0 % (Large) against 0,
+// 50 % no better (profiles/r05_mlptail_ab.txt).
 #ifndef WH_MLP_SPREAD_TAIL
-#define WH_MLP_SPREAD_TAIL 0
+#define WH_MLP_SPREAD_TAIL 25
 #endif
 constexpr int kSpreadTail = WH_MLP_SPREAD_TAIL;
 template <class N>
