@@ -31,6 +31,7 @@ from __future__ import annotations
 import json
 import os
 import shlex
+import shutil
 import subprocess
 import sys
 
@@ -69,6 +70,7 @@ def build(spec):
         os.makedirs(os.path.join(ROOT, "build_ab"), exist_ok=True)
         if "rev" in v:
             dst = os.path.join(ROOT, "build", f"rev_{v['name']}")
+            shutil.rmtree(dst, ignore_errors=True)   # objects of an earlier revision would look newer
             os.makedirs(dst, exist_ok=True)
             arch = subprocess.run(["git", "-C", ROOT, "archive", v["rev"], "rllib-warehouse_amd/csrc", "include"],
                                   check=True, capture_output=True).stdout
