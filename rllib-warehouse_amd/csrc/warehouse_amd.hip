@@ -2387,20 +2387,20 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
   } else if constexpr (FAST) {   // one step
-    // the images first and the state stores after the barrier: the row stream waits only for the
-    // step and the images (the stores read the pickup plane, which the rows do not touch)
     if (loaded) {
       run.step(a, s, L, nullptr, k, gid, e, tid, 0);
+      store_env<C>(s, L, a.state, a.B, e0, na, tid);
       write_image<C>(s, L, O, tid, C::NAM, 0);
     }
     __syncthreads();
-    if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
     write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
-    if (stepped) run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+    if (stepped) {
+      run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+      store_env<C>(s, L, a.state, a.B, e0, na, tid);
+    }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
     __syncthreads();
-    if (stepped) store_env<C>(s, L, a.state, a.B, e0, na, tid);
     write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   }
 }
