@@ -586,10 +586,18 @@ constexpr bool kSpreadL0 = kSpreadDma;
 constexpr bool kSpreadL0 = false;
 #endif
 struct NextChunk {
-  const u32x4* src;
+  int op0;    // the chunk's first operand in the packed stream
   int dst;    // LDS stage, in 16-byte units from the kernel's LDS object
   int nops;   // 0: no next chunk
 };
+// One staged operand (1 KiB) by buffer-to-LDS DMA: the packed stream as a buffer resource, the
+// operand's byte offset in an SGPR (soffset), the lane's 16 bytes by the one lane-offset VGPR every
+// piece shares -- no 64-bit address per piece (with global_load_lds each piece's address pair was
+// live across the operand stream and spread-out pieces spilled, profiles/r05_tune_ab.txt).
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t wr, u32x4* dst, int op, int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, lane * 16,
+                                           op * 1024, 0, 0);
+}
 // The last kSpreadTail % of a chunk's groups issue no pieces, so the last ones have landed when the
 // chunk ends (its vmcnt(0) before the barrier): 25 % -2.6 % (Medium) / -1.0 % (Large) against 0,
 // 50 % no better (profiles/r05_mlptail_ab.txt).
@@ -598,23 +606,22 @@ struct NextChunk {
 #endif
 constexpr int kSpreadTail = WH_MLP_SPREAD_TAIL;
 template <class N>
-__device__ __forceinline__ void stage_slice(u32x4* lds, const NextChunk& nc, int gi, int ng_all, int w, int lane) {
+__device__ __forceinline__ void stage_slice(__amdgpu_buffer_rsrc_t wr, u32x4* lds, const NextChunk& nc, int gi,
+                                            int ng_all, int w, int lane) {
   constexpr int NPW = (N::SOPS + N::WAVES - 1) / N::WAVES;   // pieces per wave, at most
   const int ng = ng_all - ng_all * kSpreadTail / 100 > 0 ? ng_all - ng_all * kSpreadTail / 100 : 1;
   if (gi >= ng) return;
   const int j0 = (gi * NPW + ng - 1) / ng, j1 = ((gi + 1) * NPW + ng - 1) / ng;
   for (int j = j0; j < j1; ++j) {
     const int o = w + N::WAVES * j;   // wave-uniform: SGPR bases, one lane offset VGPR
-    if (o < nc.nops) __builtin_amdgcn_global_load_lds(nc.src + o * 64 + lane, lds + nc.dst + o * 64, 16, 0, 0);
+    if (o < nc.nops) dma_piece(wr, lds + nc.dst + o * 64, nc.op0 + o, lane);
   }
 }
 // (the LDS destination stays an offset from the __shared__ object: a generic pointer rebuilt from
 // its low 32 bits is NULL for offset 0, and its cast to the LDS address space then yields the LDS
 // null value, not offset 0)
-__device__ __forceinline__ NextChunk uniform_chunk(const u32x4* src, int dst, int nops) {
-  const uint64_t sa = reinterpret_cast<uint64_t>(src);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sa), hi = __builtin_amdgcn_readfirstlane((uint32_t)(sa >> 32));
-  return NextChunk{reinterpret_cast<const u32x4*>(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(dst),
+__device__ __forceinline__ NextChunk uniform_chunk(int op0, int dst, int nops) {
+  return NextChunk{__builtin_amdgcn_readfirstlane(op0), __builtin_amdgcn_readfirstlane(dst),
                    __builtin_amdgcn_readfirstlane(nops)};
 }
 
@@ -626,24 +633,26 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, g = lane >> 4;
-  const u32x4* chunks = static_cast<const u32x4*>(a.packed);
   const float* gb = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.packed) + N::BIAS_OFF);
   const float* b2 = gb + N::H0 + N::H1;
   const int64_t ntask = (a.rows + N::ROWS - 1) / N::ROWS;
   const int my_tasks = (int)((ntask - blockIdx.x + gridDim.x - 1) / gridDim.x);
 
   for (int i = tid; i < N::H1; i += N::MT) b1s[i] = gb[N::H0 + i];
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.packed), (short)0, (int)N::BIAS_OFF, 0x00020000);
   auto stage_of = [&](int gg) { return lds + (gg & 1) * (N::SOPS * 64); };
   auto fetch = [&](int gg) {
     if (gg < my_tasks * N::NCH) {
-      const int c = gg % N::NCH;
-      stage_chunk<N>(chunks + N::chunk_off(c) * 64, stage_of(gg), N::chunk_ops(c), w, lane);
+      const int c = gg % N::NCH, op0 = (int)N::chunk_off(c);
+      u32x4* dst = stage_of(gg);
+      for (int o = w; o < N::chunk_ops(c); o += N::WAVES) dma_piece(wr, dst + o * 64, op0 + o, lane);
     }
   };
   auto next_of = [&](int gg) -> NextChunk {
-    if (gg >= my_tasks * N::NCH) return NextChunk{chunks, 0, 0};
+    if (gg >= my_tasks * N::NCH) return NextChunk{0, 0, 0};
     const int c = gg % N::NCH;
-    return uniform_chunk(chunks + N::chunk_off(c) * 64, (gg & 1) * (N::SOPS * 64), N::chunk_ops(c));
+    return uniform_chunk((int)N::chunk_off(c), (gg & 1) * (N::SOPS * 64), N::chunk_ops(c));
   };
   fetch(0);
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -705,7 +714,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
       for (int c = 0; c < N::L0C; ++c) {
         const int gg = base + c;
         if (!kSpreadL0) fetch(gg + 1);   // (spread: 46 more registers spilled -- layer 0's fragments are all live)
-        const NextChunk nc = kSpreadL0 ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
+        const NextChunk nc = kSpreadL0 ? next_of(gg + 1) : NextChunk{0, 0, 0};
         f32x4 acc[2][NS];
         stream_ops<N::L0OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int m = i / N::U0, k = i % N::U0, rt = k / N::KQ0, q = k % N::KQ0;
@@ -715,14 +724,14 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2) hb[c * N::L0T + m][s2] = group_frag(acc[0][s2], acc[1][s2]);
           }
-        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
+        }, [&](int gi, int ng) { stage_slice<N>(wr, lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
       for (int d = 0; d < N::L1C; ++d) {
         const int gg = base + N::L0C + d;
         if (!kSpreadDma) fetch(gg + 1);
-        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{0, 0, 0};
         // the next task's X during the last chunk (X is dead once layer 0 is done; loading it for
         // the whole of layer 1 would keep its registers live beside all of layer 0's fragments)
         if (d == N::L1C - 1 && has_next) load_x(task + gridDim.x);
@@ -739,7 +748,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
             for (int s2 = 0; s2 < NS; ++s2)
               lg[s2] = mfma16(af, group_frag_bias(acc[0][s2], acc[1][s2], b1s, 32 * u, g), lg[s2]);
           }
-        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
+        }, [&](int gi, int ng) { stage_slice<N>(wr, lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
@@ -752,7 +761,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
       for (int c = 0; c < N::L0C; ++c) {
         const int gg = base + c;
         if (!kSpreadDma) fetch(gg + 1);
-        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{0, 0, 0};
         f32x4 acc0[2][NS];
         bf16x8 hb0[NS];
         stream_ops<N::L0OPS, 4, 1>(stage_of(gg), lane, [&](int i, bf16x8 af) {
@@ -770,20 +779,20 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2) acc1[v][s2] = mfma16(af, hb0[s2], acc1[v][s2]);
           }
-        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
+        }, [&](int gi, int ng) { stage_slice<N>(wr, lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
       {
         const int gg = base + N::L0C;
         if (!kSpreadDma) fetch(gg + 1);
-        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{chunks, 0, 0};
+        const NextChunk nc = kSpreadDma ? next_of(gg + 1) : NextChunk{0, 0, 0};
         if (has_next) load_x(task + gridDim.x);
         stream_ops<N::L1OPS, 4, 1>(stage_of(gg), lane, [&](int u, bf16x8 af) {
 #pragma unroll
           for (int s2 = 0; s2 < NS; ++s2)
             lg[s2] = mfma16(af, group_frag_bias(acc1[2 * u][s2], acc1[2 * u + 1][s2], b1s, 32 * u, g), lg[s2]);
-        }, [&](int gi, int ng) { stage_slice<N>(lds, nc, gi, ng, w, lane); });
+        }, [&](int gi, int ng) { stage_slice<N>(wr, lds, nc, gi, ng, w, lane); });
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
