@@ -580,10 +580,6 @@ constexpr bool kSpreadDma = true;
 #else
 constexpr bool kSpreadDma = false;
 #endif
-#ifndef WH_MLP_L1_DEPTH   // operand groups read ahead in MODE 0's layer-1 chunks (A/B)
-#define WH_MLP_L1_DEPTH 2
-#endif
-constexpr int kL1Depth = WH_MLP_L1_DEPTH;
 #ifdef WH_MLP_SPREAD_L0   // (A/B) also in MODE 0's layer-0 chunks: Medium +13 % (spills), profiles/r05_tune_ab.txt
 constexpr bool kSpreadL0 = kSpreadDma;
 #else
@@ -720,7 +716,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
         if (!kSpreadL0) fetch(gg + 1);   // (spread: 46 more registers spilled -- layer 0's fragments are all live)
         const NextChunk nc = kSpreadL0 ? next_of(gg + 1) : NextChunk{0, 0, 0};
         f32x4 acc[2][NS];
-        stream_ops<N::L0OPS, kSpreadL0 ? 2 : 4>(stage_of(gg), lane, [&](int i, bf16x8 af) {
+        stream_ops<N::L0OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int m = i / N::U0, k = i % N::U0, rt = k / N::KQ0, q = k % N::KQ0;
 #pragma unroll
           for (int s2 = 0; s2 < NS; ++s2) acc[rt][s2] = mfma16(af, xb[q][s2], q == 0 ? f32x4{} : acc[rt][s2]);
@@ -740,7 +736,7 @@ __global__ __launch_bounds__(N::MT) void k_mlp16(MlpArgs a) {
         // the whole of layer 1 would keep its registers live beside all of layer 0's fragments)
         if (d == N::L1C - 1 && has_next) load_x(task + gridDim.x);
         f32x4 acc[2][NS];
-        stream_ops<N::L1OPS, 4, kL1Depth>(stage_of(gg), lane, [&](int i, bf16x8 af) {
+        stream_ops<N::L1OPS>(stage_of(gg), lane, [&](int i, bf16x8 af) {
           const int uu = i / N::U1, k = i % N::U1;
           if (k < 2 * N::G0) {
             const int rt = k / N::G0, m = k % N::G0;
