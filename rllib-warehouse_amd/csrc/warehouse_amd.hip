@@ -3057,9 +3057,6 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
   int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
-#ifdef WH_OBS_SEL   // (A/B builds) 0 / 1 / 2 = 8 / 16 / 64 envs per workgroup for every shape
-  sel = WH_OBS_SEL;
-#endif
   int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
   if (xfrag && (uintptr_t)xfrag % 16 != 0) return WH_EINVAL;
   // the fragment operand is written in whole 32-row tiles per workgroup: groups of 64 envs hold
