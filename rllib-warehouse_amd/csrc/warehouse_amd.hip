@@ -1571,6 +1571,7 @@ struct StepParams {
   const uint8_t* mask;      // [B] or NULL: envs to step (wh_vector_step)
   uint32_t* state_out;      // NULL: in place; else the state is read from `state`, written here
                             // (wh_sampler_step_to: double-buffered, no mask)
+  uint4* xfrag;             // (experiment) k_sampler: the fragment operand instead of f32 rows
 };
 
 // Folds the episodes this wave finished into the per-n bins of wh_episode_stats (the
@@ -2067,6 +2068,53 @@ __device__ __forceinline__ void stream_rows(const uint32_t* lims, const uint32_t
   }
 }
 
+// The same rows as the policy network's layer-0 B operand (wh_observe_x's layout, below) for the
+// group's envs [e0, e0 + nenv), from the images: NT lanes, 16 bytes of whole 32-row tiles each
+// (the group's rows nenv * na are whole tiles except in a tail group).  src0 / src1: the gather
+// tables (fresh / not fresh: lim's top bit), img: IMG bytes per env.
+template <int NT, int L, int IMG>
+__device__ __forceinline__ void stream_frags(const uint32_t* lims, const uint32_t* src0, const uint32_t* src1,
+                                             const uint8_t* img, uint4* __restrict__ xfrag, int64_t e0,
+                                             uint32_t nenv, int na, int tid) {
+  constexpr int KQ = (L + 2 + 15) / 16;
+  const uint32_t rows = nenv * (uint32_t)na, tiles = (rows + 31u) / 32u;   // (a tail group: fewer)
+  const uint32_t magic = 0xFFFFFFFFu / (uint32_t)na + 1u;   // row / na == umulhi(row, magic) (row * na < 2^32)
+  uint4* out = xfrag + ((e0 * na) / 32) * (int64_t)(KQ * 64);
+  for (uint32_t c = tid; c < tiles * KQ * 64; c += NT) {
+    const uint32_t lane = c & 63u, tq = c >> 6, q = tq % KQ, t = tq / KQ;
+    const uint32_t row = t * 32u + (lane & 31u);   // counted from the group's first env
+    const uint32_t el1 = __umulhi(row, magic), i = row - el1 * (uint32_t)na;
+    const bool rl = row < rows;
+    const uint32_t lim = lims[rl ? el1 : 0];
+    const bool live_row = rl && i < ((lim & 0x7FFFFFFFu) / L);
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>((int32_t)lim < 0 ? src1 : src0);
+    const uint8_t* im = img + (rl ? el1 : 0) * IMG;
+    // unconditional gathers (see stream_rows): the index of a padding feature (k >= L) reads a
+    // gather byte past the row, or past the table, and is selected away
+    const uint32_t k0 = 16u * q + 8u * (lane >> 5);
+    uint32_t gb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gb[j] = sb[i * L + k0 + j];
+    uint32_t w[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      uint32_t hv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t k = k0 + 2u * jj + u;
+        const float x = (float)im[gb[2 * jj + u]];
+        const float v = k < (uint32_t)L ? (live_row ? x : 0.0f) : (k < (uint32_t)L + 2u ? 1.0f : 0.0f);
+        hv[u] = __float_as_uint(v) >> 16;   // byte values and 1.0: exact in bf16
+      }
+      w[jj] = hv[0] | (hv[1] << 16);
+    }
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    const u32x4v v = {w[0], w[1], w[2], w[3]};
+    if constexpr (kObsNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(&out[c]));
+    else *reinterpret_cast<u32x4v*>(&out[c]) = v;
+  }
+}
+
 template <class C, int OBS_EB>
 struct ObsLds {
   static constexpr int IMG = (C::L + 3) & ~3;
@@ -2156,45 +2204,8 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   }
   __syncthreads();
   const uint32_t per_env = (uint32_t)na * L;
-  if (xfrag) {
-    // the group's rows are whole 32-row tiles (OBS_EB * na % 32 == 0, checked on the host)
-    constexpr int KQ = (L + 2 + 15) / 16;
-    const uint32_t rows = nenv * (uint32_t)na, tiles = (rows + 31u) / 32u;   // (a tail group: fewer)
-    uint4* out = xfrag + ((e0 * na) / 32) * (int64_t)(KQ * 64);
-    for (uint32_t c = tid; c < tiles * KQ * 64; c += BT) {
-      const uint32_t lane = c & 63u, tq = c >> 6, q = tq % KQ, t = tq / KQ;
-      const uint32_t row = t * 32u + (lane & 31u);   // counted from the group's first env
-      const uint32_t el1 = row / (uint32_t)na, i = row - el1 * (uint32_t)na;
-      const bool rl = row < rows;
-      const uint32_t lim = O.lim[rl ? el1 : 0];
-      const bool live_row = rl && i < ((lim & 0x7FFFFFFFu) / L);
-      const uint8_t* sb = reinterpret_cast<const uint8_t*>(O.src[lim >> 31]);
-      const uint8_t* im = O.img[rl ? el1 : 0];
-      // unconditional gathers (see stream_rows): the index of a padding feature (k >= L) reads a
-      // gather byte past the row, or past the table, and is selected away
-      const uint32_t k0 = 16u * q + 8u * (lane >> 5);
-      uint32_t gb[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gb[j] = sb[i * L + k0 + j];
-      uint32_t w[4];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        uint32_t hv[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint32_t k = k0 + 2u * jj + u;
-          const float x = (float)im[gb[2 * jj + u]];
-          const float v = k < (uint32_t)L ? (live_row ? x : 0.0f) : (k < (uint32_t)L + 2u ? 1.0f : 0.0f);
-          hv[u] = __float_as_uint(v) >> 16;   // byte values and 1.0: exact in bf16
-        }
-        w[jj] = hv[0] | (hv[1] << 16);
-      }
-      typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-      const u32x4v v = {w[0], w[1], w[2], w[3]};
-      if constexpr (kObsNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(&out[c]));
-      else *reinterpret_cast<u32x4v*>(&out[c]) = v;
-    }
-  }
+  if (xfrag)   // the group's rows are whole 32-row tiles (OBS_EB * na % 32 == 0, checked on the host)
+    stream_frags<BT, L, ObsLds<C, OBS_EB>::IMG>(O.lim, O.src[0], O.src[1], &O.img[0][0], xfrag, e0, nenv, na, tid);
   if (!obs) return;
   float* out = obs + e0 * per_env;
   if (quads) {
@@ -2393,7 +2404,11 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       write_image<C>(s, L, O, tid, C::NAM, 0);
     }
     __syncthreads();
-    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    if (a.xfrag)
+      stream_frags<2 * BT, C::L, SampLds<C>::IMG>(O.lim[0], O.src[0], O.src[1], &O.img[0][0][0], a.xfrag, e0,
+                                                  nenv, na, tid);
+    else
+      write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
     if (stepped) {
       run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
@@ -2401,7 +2416,11 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
     __syncthreads();
-    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    if (a.xfrag)
+      stream_frags<2 * BT, C::L, SampLds<C>::IMG>(O.lim[0], O.src[0], O.src[1], &O.img[0][0][0], a.xfrag, e0,
+                                                  nenv, na, tid);
+    else
+      write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   }
 }
 
@@ -3120,6 +3139,52 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
   rc = enqueue(l);
   if (rc || !obs) return rc;
   return wh_observe(cfg, B, state, obs, stream);
+}
+
+// wh_vector_step with the rows written as the policy network's fragment-order operand (the policy
+// route, scripts/rollout.py:72 -> env.step): the step launch, then wh_observe_x.  (k_sampler writing
+// the operand from its images in the step launch ran 1.8 % slower per policy step than the two
+// launches, profiles/r05_vsx_ab.txt: the operand's per-byte gathers at 8 waves per CU against
+// k_observe's full occupancy.)
+int wh_vector_step_x(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
+                     const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, void* xfrag,
+                     const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
+                     uint64_t seed, int64_t env_offset, void* stream) {
+  if (B > 0 && (!actions || !xfrag)) return WH_EINVAL;
+  if ((uintptr_t)xfrag % 16 != 0 || !stats_ok(stats)) return WH_EINVAL;
+  StepParams a{};
+  a.actions = actions;
+  a.order = order;
+  a.mask = mask;
+  a.rewards = rewards;
+  a.dones = dones;
+  a.k0 = (uint32_t)(seed & 0xFFFFFFFFu);
+  a.k1 = (uint32_t)(seed >> 32);
+  a.env_offset = env_offset;
+  a.steps = 1;
+  a.phase = PH_ALL;
+  a.autoreset = autoreset ? 1 : 0;
+  a.variable_n = variable_n ? 1 : 0;
+  if (stats) a.stats = *stats;
+  wh_launch l;
+  int rc = resolve_step(cfg, B, state, POL_EXTERNAL, a, stream, &l);
+  if (rc) return rc;
+  if (B == 0) return WH_OK;
+  static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
+  Geometry g;
+  const Kernels* k = nullptr;
+  const uint32_t* tab = nullptr;
+  if (!unfused && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && fuse_rows(g)) {
+    void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
+    if (fused_ok(fk)) {
+      l.a.xfrag = static_cast<uint4*>(xfrag);
+      hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, nullptr);
+      return hip_err(hipGetLastError());
+    }
+  }
+  rc = enqueue(l);
+  if (rc) return rc;
+  return wh_observe_x(cfg, B, state, nullptr, xfrag, stream);
 }
 
 int wh_sampler_step(const wh_config* cfg, int64_t B, uint32_t* state, int32_t policy, float p,

@@ -35,7 +35,7 @@ SYMBOLS = ("wh_query", "wh_pack", "wh_unpack", "wh_reset", "wh_step", "wh_observ
            "wh_rollout", "wh_vector_step", "wh_mlp_query", "wh_mlp_pack", "wh_mlp_forward", "wh_version",
            "wh_observe_x", "wh_mlp_forward_x",
            "wh_check_read", "wh_rollout_prepare", "wh_launch_run", "wh_launch_run_timed", "wh_launch_free",
-           "wh_sampler_step", "wh_sampler_step_to", "wh_sampler_rollout")
+           "wh_sampler_step", "wh_sampler_step_to", "wh_sampler_rollout", "wh_vector_step_x")
 
 
 class WhConfig(ctypes.Structure):
@@ -141,6 +141,7 @@ def lib() -> ctypes.CDLL:
     _ST = ctypes.POINTER(WhEpisodeStats)
     S.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     S.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    S.wh_vector_step_x.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     S.wh_sampler_step.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]
     S.wh_sampler_step_to.argtypes = [_CFG, _I64, _P, _P, _I32, _F32, _P, _P, _ST, _I32, _U64, _I64, _P]
     S.wh_sampler_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]

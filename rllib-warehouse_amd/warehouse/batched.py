@@ -221,14 +221,18 @@ class BatchedWarehouse:
         self._call("wh_observe", self.state.data_ptr(), self._obs.data_ptr(), self.stream)
         return self._obs
 
-    def observe_x(self, obs: bool = False):
-        """The observation rows as the policy network's layer-0 operand (wh_observe_x: bf16, MFMA
-        fragment order, for MLPPolicy.forward_x), optionally also the f32 rows.  Returns the
-        env-owned uint8 buffer [tiles, KQ, 64, 16] (and the obs tensor when obs=True)."""
+    def _xfrag_buffer(self) -> torch.Tensor:
         kq = (self.obs_len + 2 + 15) // 16
         tiles = (self.B * self.agent_slots + 31) // 32
         if getattr(self, "_xfrag", None) is None or self._xfrag.shape[0] != tiles:
             self._xfrag = torch.empty((tiles, kq, 64, 16), dtype=torch.uint8, device=self.device)
+        return self._xfrag
+
+    def observe_x(self, obs: bool = False):
+        """The observation rows as the policy network's layer-0 operand (wh_observe_x: bf16, MFMA
+        fragment order, for MLPPolicy.forward_x), optionally also the f32 rows.  Returns the
+        env-owned uint8 buffer [tiles, KQ, 64, 16] (and the obs tensor when obs=True)."""
+        self._xfrag_buffer()
         if obs and self._obs is None:
             self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
                                     device=self.device)
@@ -259,6 +263,22 @@ class BatchedWarehouse:
                    self.dones.data_ptr(), nat.ptr(obs), None if self.stats is None else self.stats.ref,
                    int(bool(autoreset)), int(self.train), self.seed, self.env_offset, self.stream)
         return obs, self.rewards, self.dones
+
+    def vector_step_x(self, actions, autoreset: bool = True, mask=None, order=None):
+        """vector_step with the rows written as the policy network's fragment-order operand
+        (wh_vector_step_x: the step launch writes observe_x()'s buffer itself).  Returns env-owned
+        (fragments [tiles, KQ, 64, 16] uint8, rewards [B,NA], dones [B])."""
+        a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
+        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        xf = self._xfrag_buffer()
+        self._call("wh_vector_step_x", self.state.data_ptr(), a.data_ptr(), nat.ptr(o), nat.ptr(m),
+                   self.rewards.data_ptr(), self.dones.data_ptr(), xf.data_ptr(),
+                   None if self.stats is None else self.stats.ref, int(bool(autoreset)), int(self.train),
+                   self.seed, self.env_offset, self.stream)
+        return xf, self.rewards, self.dones
 
     def sampler_step(self, policy: str = "greedy", p: float = 0.0, observe: bool = True
                      ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:

@@ -669,6 +669,38 @@ def test_sampler_observation_rows_equal_wh_observe(wh, variant, na, train, B):
 
 
 
+@pytest.mark.parametrize("variant,na,train,B", [("medium", 8, False, 4096), ("medium", 9, True, 1000),
+                                                ("large", 16, False, 777), ("small", 4, True, 2049),
+                                                ("small", 3, False, 129)])
+def test_vector_step_x_equals_vector_step_then_observe_x(wh, variant, na, train, B):
+    """wh_vector_step_x (the step launch writing the policy's fragment-order operand) == the same
+    wh_vector_step without rows followed by wh_observe_x, byte for byte, with equal rewards, dones
+    and states: the fast instance (every env stepped, ascending order), masked steps and dict order
+    (the generic instance), ragged batches, odd agent counts, Train variants, Large-16 (two
+    launches: its step code does not fit the fused launch)."""
+    import torch
+
+    a = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=3)
+    b = wh.BatchedWarehouse(variant, B, None if train else na, train=train, seed=3)
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=a.device).manual_seed(1)
+    NA = a.agent_slots
+    for s in range(230):
+        acts = torch.randint(0, 9, (B, NA), device=a.device, dtype=torch.int32, generator=g)
+        mask = (torch.rand(B, device=a.device, generator=g) < 0.5) if s % 5 == 1 else None
+        order = None
+        if s % 7 == 3:
+            order = torch.argsort(torch.rand((B, NA), device=a.device, generator=g), dim=1).to(torch.int32)
+        xa, ra, da = a.vector_step_x(acts, autoreset=True, mask=mask, order=order)
+        _, rb, db = b.vector_step(acts, autoreset=True, observe=False, mask=mask, order=order)
+        xb = b.observe_x()
+        assert torch.equal(xa, xb), f"step {s}"
+        keep = torch.ones(B, dtype=torch.bool, device=a.device) if mask is None else mask
+        assert torch.equal(ra[keep], rb[keep]) and torch.equal(da[keep], db[keep]), f"step {s}"
+        assert torch.equal(a.state, b.state), f"step {s}"
+
+
 @pytest.mark.parametrize("variant,na,train,p,graph", [("medium", 8, False, 0.0, False), ("medium", 9, True, 0.2, False),
                                                       ("large", 16, False, 0.0, True), ("small", 4, True, 0.1, True)])
 def test_sampler_pipeline_equals_sampler_step(wh, variant, na, train, p, graph):
