@@ -617,7 +617,7 @@ def measure_sampler_pipeline(env, K, W, dev, world, dist):
 
 def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
     """scripts/rollout.py's loop on the device: per step the SAC policy network
-    (wh_mlp_forward, argmax) over all B x NA observation rows, then one step launch (step +
+    (wh_mlp_forward, argmax) over all B x NA observation rows, then the step (step +
     auto-reset + next rows: wh_vector_step_x for the bf16 network's fragment operand,
     wh_vector_step's f32 rows for the f32 network).  hipGraph of G steps.  Returns (elapsed_s, mlp_kernel_ms, net)."""
     import torch
@@ -642,7 +642,7 @@ def measure_policy(env, K, W, dev, world, dist, precision="bf16"):
 
     def one():
         infer()
-        if frag:   # the step launch writes the next operand itself (wh_vector_step_x)
+        if frag:   # step + the next operand (wh_vector_step_x)
             env.vector_step_x(acts, autoreset=True)
         else:
             env.vector_step(acts, autoreset=True, observe=True)
@@ -942,8 +942,8 @@ def main():
             line = {
                 "workload": f"scripts/rollout.py loop on device: SAC policy_model MLP [{net.in_dim},{net.hidden[0]},"
                             f"{net.hidden[1]},9] argmax over B*NA={rows} rows -> "
-                            + ("wh_vector_step_x (step + auto-reset + the observation rows as the MLP's bf16 "
-                               "fragment-order operand, one launch)" if prec == "bf16"
+                            + ("wh_vector_step_x (step + auto-reset, then the observation rows as the MLP's bf16 "
+                               "fragment-order operand)" if prec == "bf16"
                                else "wh_vector_step (step + auto-reset + f32 observation rows)") +
                             "; random-init weights (no checkpoint ships with the reference)",
                 "value": aggregate_rate(world, B, NA, Kp, el4), "unit": "agent-steps/s", "steps": Kp,

@@ -186,10 +186,10 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
                    uint64_t seed, int64_t env_offset, void* stream);
 
 /* wh_vector_step writing the rows as wh_observe_x's fragment-order operand (xfrag, 16-byte
- * aligned, [ceil(B*NA/32), KQ, 64, 16] bytes, KQ = (9R+1+2+15)/16) instead of f32 rows: the policy
- * route of scripts/rollout.py:72 (network forward on the operand -> env.step -> next operand) with
- * the operand written by the step launch itself.  The same transitions and the same operand bytes
- * as wh_vector_step(obs = NULL) followed by wh_observe_x. */
+ * aligned, [ceil(B*NA/32), KQ, 64, 16] bytes, KQ = (9R+1+2+15)/16) instead of f32 rows: the step of
+ * the policy route of scripts/rollout.py:72 (network forward on the operand -> env.step -> next
+ * operand).  The same transitions and operand bytes as wh_vector_step(obs = NULL) followed by
+ * wh_observe_x (which is what it runs). */
 int wh_vector_step_x(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
                      const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, void* xfrag,
                      const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,

@@ -1571,7 +1571,6 @@ struct StepParams {
   const uint8_t* mask;      // [B] or NULL: envs to step (wh_vector_step)
   uint32_t* state_out;      // NULL: in place; else the state is read from `state`, written here
                             // (wh_sampler_step_to: double-buffered, no mask)
-  uint4* xfrag;             // (experiment) k_sampler: the fragment operand instead of f32 rows
 };
 
 // Folds the episodes this wave finished into the per-n bins of wh_episode_stats (the
@@ -2404,11 +2403,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       write_image<C>(s, L, O, tid, C::NAM, 0);
     }
     __syncthreads();
-    if (a.xfrag)
-      stream_frags<2 * BT, C::L, SampLds<C>::IMG>(O.lim[0], O.src[0], O.src[1], &O.img[0][0][0], a.xfrag, e0,
-                                                  nenv, na, tid);
-    else
-      write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
     if (stepped) {
       run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
@@ -2416,11 +2411,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
     __syncthreads();
-    if (a.xfrag)
-      stream_frags<2 * BT, C::L, SampLds<C>::IMG>(O.lim[0], O.src[0], O.src[1], &O.img[0][0][0], a.xfrag, e0,
-                                                  nenv, na, tid);
-    else
-      write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   }
 }
 
@@ -3170,18 +3161,6 @@ int wh_vector_step_x(const wh_config* cfg, int64_t B, uint32_t* state, const int
   int rc = resolve_step(cfg, B, state, POL_EXTERNAL, a, stream, &l);
   if (rc) return rc;
   if (B == 0) return WH_OK;
-  static const bool unfused = getenv("WH_SAMPLER_UNFUSED") != nullptr;
-  Geometry g;
-  const Kernels* k = nullptr;
-  const uint32_t* tab = nullptr;
-  if (!unfused && prepare(cfg, B, stream, &g, &k, &tab) == WH_OK && fuse_rows(g)) {
-    void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
-    if (fused_ok(fk)) {
-      l.a.xfrag = static_cast<uint4*>(xfrag);
-      hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, nullptr);
-      return hip_err(hipGetLastError());
-    }
-  }
   rc = enqueue(l);
   if (rc) return rc;
   return wh_observe_x(cfg, B, state, nullptr, xfrag, stream);

@@ -266,7 +266,7 @@ class BatchedWarehouse:
 
     def vector_step_x(self, actions, autoreset: bool = True, mask=None, order=None):
         """vector_step with the rows written as the policy network's fragment-order operand
-        (wh_vector_step_x: the step launch writes observe_x()'s buffer itself).  Returns env-owned
+        (wh_vector_step_x: the step, then observe_x()'s buffer).  Returns env-owned
         (fragments [tiles, KQ, 64, 16] uint8, rewards [B,NA], dones [B])."""
         a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
         o = _dev_i32(order, self.device, (self.B, self.agent_slots))

@@ -117,10 +117,10 @@ def policy_rollout(env, net: MLPPolicy, steps: int, *, explore: bool = False, se
                    first_step: int = 0, record=None, operand: str = "auto"):
     """scripts/rollout.py's loop (compute_action per agent -> env.step, until done) for every env
     of a BatchedWarehouse, on the device: per step one network forward over all B x NA observation
-    rows, then one step launch (step + auto-reset + the next rows).  operand="fragments" (the
-    default for bf16 networks) hands the rows to the network as its layer-0 operand
-    (wh_vector_step_x writes it from the step launch, wh_mlp_forward_x reads it: the same actions,
-    no f32 rows materialised); "rows" uses the float32 observation rows (wh_vector_step).  `record`, if given, is called as record(step, actions, rewards,
+    rows, then the step (step + auto-reset + the next rows).  operand="fragments" (the default for
+    bf16 networks) hands the rows to the network as its layer-0 operand (wh_vector_step_x writes
+    it, wh_mlp_forward_x reads it: the same actions, no f32 rows materialised); "rows" uses the
+    float32 observation rows (wh_vector_step).  `record`, if given, is called as record(step, actions, rewards,
     dones) with env-owned device tensors.  Returns the last step's observations (the fragment
     buffer or the obs tensor)."""
     if operand == "auto":
@@ -134,7 +134,7 @@ def policy_rollout(env, net: MLPPolicy, steps: int, *, explore: bool = False, se
     for s in range(steps):
         if frag:
             net.forward_x(obs, B * NA, explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
-            obs, rew, done = env.vector_step_x(acts, autoreset=True)   # step + next operand, one launch
+            obs, rew, done = env.vector_step_x(acts, autoreset=True)   # step + the next operand
         else:
             net(obs.view(B * NA, -1), explore=explore, seed=seed, step=first_step + s, actions=acts.view(-1))
             obs, rew, done = env.vector_step(acts, autoreset=True, observe=True)
