@@ -2141,41 +2141,79 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C, OBS_EB>::SRCW;
   constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
   const int tid = threadIdx.x;
-  const uint32_t* srcg = &kObsSrc<C::R, C::NAM>.w[0][0];
-  for (int k = tid; k < 2 * SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
-  for (int k = tid; k < C::P; k += BT) O.rp[k] = tables[C::T.rp / 4 + 2 * k];
-  for (int k = tid; k < C::DP; k += BT) O.dst[k] = tables[C::T.dst / 4 + k];
-
   const int64_t e0 = (int64_t)blockIdx.x * OBS_EB;
   const uint32_t nenv = (uint32_t)((B - e0) < OBS_EB ? (B - e0) : OBS_EB);
   const int el = tid / OBS_PARTS, part = tid % OBS_PARTS;
   const bool mine = (uint32_t)el < nenv;
   const int64_t e = e0 + el;
-  const uint8_t nul = (uint8_t)(D / 2);
-  uint32_t n = 0;
-  bool fresh = false;
+  // Every global load of the prologue is issued before its first use: as strided loops, each
+  // iteration compiled to a load -> vmcnt(0) -> LDS write round trip, and the agent rows waited on
+  // the header (their guard was r < n) -- about eight serial memory latencies per workgroup for
+  // Large-16 (five for its 4.6 KB gather table alone), now one.  An agent row past n is loaded and
+  // replaced by IDLE below (rows r < na exist in the state).
+  constexpr int NSRC = (2 * SRCW + BT - 1) / BT, NRP = (C::P + BT - 1) / BT, NDP = (C::DP + BT - 1) / BT;
+  constexpr int NAR = (R + OBS_PARTS - 1) / OBS_PARTS, NPW = (C::PW + OBS_PARTS - 1) / OBS_PARTS;
+  const uint32_t* srcg = &kObsSrc<C::R, C::NAM>.w[0][0];
+  uint32_t sv[NSRC], rv[NRP], dv[NDP], av[NAR], pv[NPW], hdr = 0;
+#pragma unroll
+  for (int i = 0; i < NSRC; ++i) sv[i] = tid + i * BT < 2 * SRCW ? srcg[tid + i * BT] : 0u;
+#pragma unroll
+  for (int i = 0; i < NRP; ++i) rv[i] = tid + i * BT < C::P ? tables[C::T.rp / 4 + 2 * (tid + i * BT)] : 0u;
+#pragma unroll
+  for (int i = 0; i < NDP; ++i) dv[i] = tid + i * BT < C::DP ? tables[C::T.dst / 4 + tid + i * BT] : 0u;
   if (mine) {
-    const uint32_t hdr = state[e];
-    n = (hdr >> 16) & 0xFFu;
+    hdr = state[e];
+#pragma unroll
+    for (int i = 0; i < NAR; ++i) {
+      const int r = part + i * OBS_PARTS;
+      av[i] = (r < R && r < na) ? state[(2 + r) * B + e] : IDLE;
+    }
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int w = part + i * OBS_PARTS;
+      pv[i] = w < C::PW ? state[(2 + na + w) * B + e] : 0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NSRC; ++i)
+    if (tid + i * BT < 2 * SRCW) (&O.src[0][0])[tid + i * BT] = sv[i];
+#pragma unroll
+  for (int i = 0; i < NRP; ++i)
+    if (tid + i * BT < C::P) O.rp[tid + i * BT] = rv[i];
+#pragma unroll
+  for (int i = 0; i < NDP; ++i)
+    if (tid + i * BT < C::DP) O.dst[tid + i * BT] = dv[i];
+
+  const uint8_t nul = (uint8_t)(D / 2);
+  if (mine) {
+    uint32_t n = (hdr >> 16) & 0xFFu;
     n = n < (uint32_t)na ? n : (uint32_t)na;
-    fresh = (hdr >> 24) & 1u;
+    const bool fresh = (hdr >> 24) & 1u;
     uint8_t* im = O.img[el];
     if (part == 0) {
       im[0] = (uint8_t)n;
       O.lim[el] = n * L | (fresh ? 0x80000000u : 0u);
     }
-    for (int r = part; r < R; r += OBS_PARTS) {          // agent rows
-      const bool live = r < (int)n;
-      const uint32_t a = live ? state[(2 + r) * B + e] : IDLE;
-      const bool carry = (a & 0xFF00u) != 0xFF00u;
-      im[A0 + r] = (uint8_t)((live && !fresh && !carry) ? 1 : 0);
-      const bool show = live && !fresh && carry;
-      im[G0 + 2 * r] = show ? (uint8_t)((a >> 8) & 0xFFu) : nul;
-      im[G0 + 2 * r + 1] = show ? (uint8_t)(a >> 24) : nul;
-      im[P0 + 2 * r] = live ? (uint8_t)(a & 0xFFu) : nul;
-      im[P0 + 2 * r + 1] = live ? (uint8_t)((a >> 16) & 0xFFu) : nul;
+#pragma unroll
+    for (int i = 0; i < NAR; ++i) {                       // agent rows
+      const int r = part + i * OBS_PARTS;
+      if (r < R) {
+        const bool live = r < (int)n;
+        const uint32_t a = live ? av[i] : IDLE;
+        const bool carry = (a & 0xFF00u) != 0xFF00u;
+        im[A0 + r] = (uint8_t)((live && !fresh && !carry) ? 1 : 0);
+        const bool show = live && !fresh && carry;
+        im[G0 + 2 * r] = show ? (uint8_t)((a >> 8) & 0xFFu) : nul;
+        im[G0 + 2 * r + 1] = show ? (uint8_t)(a >> 24) : nul;
+        im[P0 + 2 * r] = live ? (uint8_t)(a & 0xFFu) : nul;
+        im[P0 + 2 * r + 1] = live ? (uint8_t)((a >> 16) & 0xFFu) : nul;
+      }
     }
-    for (int w = part; w < C::PW; w += OBS_PARTS) O.ptw[el][w] = state[(2 + na + w) * B + e];
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int w = part + i * OBS_PARTS;
+      if (w < C::PW) O.ptw[el][w] = pv[i];
+    }
   }
   __syncthreads();
   if (mine) {                                             // requests: ascending pickup index
