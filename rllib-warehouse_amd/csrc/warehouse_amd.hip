@@ -2399,8 +2399,15 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     commit_table_chunk<C>(L.tbl, 0, tv0);
     commit_table_chunk<C>(L.tbl, 1, tv1);
   } else {
+    // all loads first, then the LDS writes: one memory latency, not one per strided iteration
     const uint32_t* srcg = &kObsSrcF<C::R, C::NAM>.w[0][0];
-    for (int k = tid - BT; k < 2 * SampLds<C>::SRCW; k += BT) (&O.src[0][0])[k] = srcg[k];
+    constexpr int NS = 2 * SampLds<C>::SRCW, NSRC = (NS + BT - 1) / BT;
+    uint32_t sv[NSRC];
+#pragma unroll
+    for (int i = 0; i < NSRC; ++i) sv[i] = tid - BT + i * BT < NS ? srcg[tid - BT + i * BT] : 0u;
+#pragma unroll
+    for (int i = 0; i < NSRC; ++i)
+      if (tid - BT + i * BT < NS) (&O.src[0][0])[tid - BT + i * BT] = sv[i];
   }
   __syncthreads();
   const uint32_t nenv = (uint32_t)((a.B - e0) < BT ? (a.B - e0) : BT);
