@@ -71,6 +71,11 @@ constexpr bool kBiasAddr = false;
 #endif
 // -DWH_OBS_NT: observation rows stored nontemporal (A/B: 5 % slower at Medium-8 and Large-16, 5 %
 // faster at Small-4, same box; tools/obs_bench.py)
+// -DWH_OBS_EB0=<n>: envs per workgroup of the observation kernel for the widest rows (Large)
+#ifndef WH_OBS_EB0
+#define WH_OBS_EB0 8
+#endif
+constexpr int kObsEB0 = WH_OBS_EB0;
 #ifdef WH_OBS_NT
 constexpr bool kObsNT = true;
 #else
@@ -2685,7 +2690,7 @@ struct Kernels {
   void (*sampler_multi[3])(StepParams, float*);   // [policy]: the same, K steps per launch (greedy / random)
   void (*vsampler[2])(StepParams, float*);  // [ordered]: wh_vector_step's step + rows (external actions)
   void (*reset)(ResetParams);
-  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // 8 / 16 / 64 envs per WG
+  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // kObsEB0 / 16 / 64 envs per WG
   int tblw, nv;
 };
 
@@ -2720,7 +2725,7 @@ Kernels make_kernels() {
   k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
   k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
-  k.observe[0] = k_observe<C, 8>;
+  k.observe[0] = k_observe<C, kObsEB0>;
   k.observe[1] = k_observe<C, 16>;
   k.observe[2] = k_observe<C, 64>;
   k.tblw = C::TBLW;
@@ -3112,7 +3117,7 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
   int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
-  int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : 8);
+  int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : kObsEB0);
   if (xfrag && (uintptr_t)xfrag % 16 != 0) return WH_EINVAL;
   // the fragment operand is written in whole 32-row tiles per workgroup: groups of 64 envs hold
   // 64 * NA rows, a multiple of 32 for every agent count (e.g. Medium with 9 agents, whose f32-row
