@@ -73,7 +73,7 @@ constexpr bool kBiasAddr = false;
 // faster at Small-4, same box; tools/obs_bench.py)
 // -DWH_OBS_EB0=<n>: envs per workgroup of the observation kernel for the widest rows (Large)
 #ifndef WH_OBS_EB0
-#define WH_OBS_EB0 8
+#define WH_OBS_EB0 4
 #endif
 constexpr int kObsEB0 = WH_OBS_EB0;
 #ifdef WH_OBS_NT
@@ -3113,10 +3113,13 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   if (B == 0) return WH_OK;
   if (!state || (!obs && !xfrag)) return WH_EINVAL;
   const int quads = ((g.NA * (9 * g.R + 1)) % 4 == 0) && ((uintptr_t)obs % 16 == 0);
-  // envs per workgroup: ~40-75 KB of rows per group (measured: 64 for Small-4's 592 B/env rows,
-  // 16 for Medium-8's 2.6 KB, 8 for Large-16's 9.3 KB; tools/obs_bench.py)
+  // envs per workgroup (same-box A/Bs, tools/obs_bench.py and tools/sampler_probe.py): f32 rows 64
+  // for Small-4's 592 B/env rows, 16 for Medium-8's 2.6 KB, 4 for Large-16's 9.3 KB
+  // (profiles/r05_obseb0_ab.txt: 8 -> 4 is 119.5 -> 115.2 us, and 133 -> 130 us for the sampler
+  // route); the fragment operand alone 64 / 16 / 16 (Large-16: 16 for 8 in profiles/r05_obseb_ab.txt,
+  // 4 is 20 % slower than 8)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
-  int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 ? 1 : 0);
+  int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 || !obs ? 1 : 0);
   int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : kObsEB0);
   if (xfrag && (uintptr_t)xfrag % 16 != 0) return WH_EINVAL;
   // the fragment operand is written in whole 32-row tiles per workgroup: groups of 64 envs hold
