@@ -71,11 +71,11 @@ constexpr bool kBiasAddr = false;
 #endif
 // -DWH_OBS_NT: observation rows stored nontemporal (A/B: 5 % slower at Medium-8 and Large-16, 5 %
 // faster at Small-4, same box; tools/obs_bench.py)
-// -DWH_OBS_EB0=<n>: envs per workgroup of the observation kernel for the widest rows (Large)
+// -DWH_OBS_EB0=<n>: envs per workgroup of the observation kernel for the widest f32 rows (Large)
 #ifndef WH_OBS_EB0
 #define WH_OBS_EB0 4
 #endif
-constexpr int kObsEB0 = WH_OBS_EB0;
+constexpr int kObsEB[4] = {WH_OBS_EB0, 8, 16, 64};   // the observation kernel's instances
 #ifdef WH_OBS_NT
 constexpr bool kObsNT = true;
 #else
@@ -2690,7 +2690,7 @@ struct Kernels {
   void (*sampler_multi[3])(StepParams, float*);   // [policy]: the same, K steps per launch (greedy / random)
   void (*vsampler[2])(StepParams, float*);  // [ordered]: wh_vector_step's step + rows (external actions)
   void (*reset)(ResetParams);
-  void (*observe[3])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // kObsEB0 / 16 / 64 envs per WG
+  void (*observe[4])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // kObsEB[i] envs per WG
   int tblw, nv;
 };
 
@@ -2725,9 +2725,10 @@ Kernels make_kernels() {
   k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
   k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
   k.reset = k_reset<C>;
-  k.observe[0] = k_observe<C, kObsEB0>;
-  k.observe[1] = k_observe<C, 16>;
-  k.observe[2] = k_observe<C, 64>;
+  k.observe[0] = k_observe<C, kObsEB[0]>;
+  k.observe[1] = k_observe<C, kObsEB[1]>;
+  k.observe[2] = k_observe<C, kObsEB[2]>;
+  k.observe[3] = k_observe<C, kObsEB[3]>;
   k.tblw = C::TBLW;
   k.nv = C::NV;
   return k;
@@ -3116,19 +3117,16 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   // envs per workgroup (same-box A/Bs, tools/obs_bench.py and tools/sampler_probe.py): f32 rows 64
   // for Small-4's 592 B/env rows, 16 for Medium-8's 2.6 KB, 4 for Large-16's 9.3 KB
   // (profiles/r05_obseb0_ab.txt: 8 -> 4 is 119.5 -> 115.2 us, and 133 -> 130 us for the sampler
-  // route); the fragment operand alone 64 / 16 / 16 (Large-16: 16 for 8 in profiles/r05_obseb_ab.txt,
-  // 4 is 20 % slower than 8)
+  // route, profiles/r05_obseb1_ab.txt 120.6 -> 114.8 us); the fragment operand alone 64 / 16 / 8
+  // (Large-16: 16 is 3 % and 4 is 20 % slower than 8, profiles/r05_obseb1_ab.txt / r05_obseb0_ab.txt)
   const int row_bytes = 4 * g.NA * (9 * g.R + 1);
-  int sel = row_bytes <= 1024 ? 2 : (row_bytes <= 4096 || !obs ? 1 : 0);
-  int ebx = sel == 2 ? 64 : (sel == 1 ? 16 : kObsEB0);
+  int sel = row_bytes <= 1024 ? 3 : (row_bytes <= 4096 ? 2 : (obs ? 0 : 1));
   if (xfrag && (uintptr_t)xfrag % 16 != 0) return WH_EINVAL;
   // the fragment operand is written in whole 32-row tiles per workgroup: groups of 64 envs hold
   // 64 * NA rows, a multiple of 32 for every agent count (e.g. Medium with 9 agents, whose f32-row
   // grouping of 16 envs = 144 rows does not)
-  if (xfrag && (ebx * g.NA) % 32 != 0) {
-    sel = 2;
-    ebx = 64;
-  }
+  if (xfrag && (kObsEB[sel] * g.NA) % 32 != 0) sel = 3;
+  const int ebx = kObsEB[sel];
   hipLaunchKernelGGL(k->observe[sel], dim3((unsigned)((B + ebx - 1) / ebx)), dim3(BT), 0,
                      (hipStream_t)stream, state, B, g.NA, tab, obs, quads, static_cast<uint4*>(xfrag));
   return hip_err(hipGetLastError());
