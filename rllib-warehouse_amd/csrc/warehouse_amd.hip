@@ -2739,6 +2739,8 @@ const std::vector<Kernels>& registry() {
   static const std::vector<Kernels> r = {make_kernels<16, 9, 3, 8>()};
 #elif defined(WH_ONLY_LARGE16)
   static const std::vector<Kernels> r = {make_kernels<20, 16, 4, 16>()};
+#elif defined(WH_ONLY_SMALL4)
+  static const std::vector<Kernels> r = {make_kernels<12, 4, 2, 4>()};
 #else
   static const std::vector<Kernels> r = {
       // WarehouseSmall  (variants.py:19-32): D=12, R=4, racks [4, 8]
