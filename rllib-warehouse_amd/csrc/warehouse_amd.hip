@@ -69,17 +69,31 @@ constexpr bool kBiasAddr = true;
 #else
 constexpr bool kBiasAddr = false;
 #endif
-// -DWH_OBS_NT: observation rows stored nontemporal (A/B: 5 % slower at Medium-8 and Large-16, 5 %
-// faster at Small-4, same box; tools/obs_bench.py)
 // -DWH_OBS_EB0=<n>: envs per workgroup of the observation kernel for the widest f32 rows (Large)
 #ifndef WH_OBS_EB0
 #define WH_OBS_EB0 4
 #endif
 constexpr int kObsEB[4] = {WH_OBS_EB0, 8, 16, 64};   // the observation kernel's instances
-#ifdef WH_OBS_NT
-constexpr bool kObsNT = true;
+// Observation stores: nontemporal for the fragment operand everywhere, and for f32 rows of <= 1 KB
+// or > 4 KB per env (Small / Large); plain for Medium's rows (same-box A/Bs, tools/obs_bench.py and
+// tools/sampler_probe.py, profiles/r05_ntm8_ab.txt and r05_l16rows_ab.txt: nontemporal rows at
+// Medium-8 +10 % observe, +24 % sampler step; at Small-4 -6 % / -1.5 %; at Large-16 -4 % observe,
+// -4 % sampler route; the operand -6 % / -9 % / -10 %).  -DWH_OBS_NT: every row store nontemporal,
+// -DWH_OBS_NO_NT: no store nontemporal (A/B switches).
+template <class C>
+constexpr bool rows_nt() {
+#if defined(WH_OBS_NT)
+  return true;
+#elif defined(WH_OBS_NO_NT)
+  return false;
 #else
-constexpr bool kObsNT = false;
+  return C::NAM * C::L * 4 <= 1024 || C::NAM * C::L * 4 > 4096;
+#endif
+}
+#ifdef WH_OBS_NO_NT
+constexpr bool kFragNT = false;
+#else
+constexpr bool kFragNT = true;
 #endif
 
 #ifndef WH_REV_SPLIT_MAX_NAM   // agent counts up to which the move loop has the no-reverse-key variant
@@ -2035,7 +2049,7 @@ __constant__ ObsSrc<R, NAM> kObsSrc = make_obs_src<R, NAM>();
 #ifndef WH_ROWS_RU
 #define WH_ROWS_RU 2
 #endif
-template <int NT, int IMG>
+template <int NT, int IMG, bool NTS>
 __device__ __forceinline__ void stream_rows(const uint32_t* lims, const uint32_t* src0, const uint32_t* src1,
                                             const uint8_t* img, f32x4* __restrict__ out4, uint32_t nenv,
                                             uint32_t qe, int tid, uint32_t q0 = 0, uint32_t q1 = ~0u) {
@@ -2065,7 +2079,7 @@ __device__ __forceinline__ void stream_rows(const uint32_t* lims, const uint32_t
     for (int u = 0; u < RU; ++u) {
       const uint32_t qu = q + (uint32_t)u * NT;
       if (u == 0 || qu < total) {
-        if constexpr (kObsNT) __builtin_nontemporal_store(v[u], &out4[qu]);
+        if constexpr (NTS) __builtin_nontemporal_store(v[u], &out4[qu]);
         else out4[qu] = v[u];
       }
     }
@@ -2114,7 +2128,7 @@ __device__ __forceinline__ void stream_frags(const uint32_t* lims, const uint32_
     }
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     const u32x4v v = {w[0], w[1], w[2], w[3]};
-    if constexpr (kObsNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(&out[c]));
+    if constexpr (kFragNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(&out[c]));
     else *reinterpret_cast<u32x4v*>(&out[c]) = v;
   }
 }
@@ -2252,7 +2266,7 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   float* out = obs + e0 * per_env;
   if (quads) {
     // per_env % 4 == 0 and obs 16-byte aligned (checked on the host)
-    stream_rows<BT, ObsLds<C, OBS_EB>::IMG>(O.lim, O.src[0], O.src[1], &O.img[0][0], reinterpret_cast<f32x4*>(out),
+    stream_rows<BT, ObsLds<C, OBS_EB>::IMG, rows_nt<C>()>(O.lim, O.src[0], O.src[1], &O.img[0][0], reinterpret_cast<f32x4*>(out),
                                             nenv, per_env >> 2, tid);
   } else {
     const uint32_t total = nenv * per_env;
@@ -2361,7 +2375,7 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
 template <class C, int NBUF>
 __device__ __forceinline__ void write_rows(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
                                            uint32_t nenv, uint32_t qe, int tid) {
-  stream_rows<2 * BT, SampLds<C, NBUF>::IMG>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
+  stream_rows<2 * BT, SampLds<C, NBUF>::IMG, rows_nt<C>()>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
                                              reinterpret_cast<f32x4*>(rows), nenv, qe, tid);
 }
 
