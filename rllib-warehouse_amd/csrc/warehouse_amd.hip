@@ -74,12 +74,14 @@ constexpr bool kBiasAddr = false;
 #define WH_OBS_EB0 4
 #endif
 constexpr int kObsEB[4] = {WH_OBS_EB0, 8, 16, 64};   // the observation kernel's instances
-// Observation stores: nontemporal for the fragment operand everywhere, and for f32 rows of <= 1 KB
-// or > 4 KB per env (Small / Large); plain for Medium's rows (same-box A/Bs, tools/obs_bench.py and
-// tools/sampler_probe.py, profiles/r05_ntm8_ab.txt and r05_l16rows_ab.txt: nontemporal rows at
-// Medium-8 +10 % observe, +24 % sampler step; at Small-4 -6 % / -1.5 %; at Large-16 -4 % observe,
-// -4 % sampler route; the operand -6 % / -9 % / -10 %).  -DWH_OBS_NT: every row store nontemporal,
-// -DWH_OBS_NO_NT: no store nontemporal (A/B switches).
+// Observation stores (same-box A/Bs, tools/obs_bench.py, sampler_probe.py and policy_probe.py;
+// profiles/r05_l16rows_ab.txt, r05_ntm8_ab.txt, r05_ntsel_ab.txt): f32 rows nontemporal for rows of
+// <= 1 KB or > 4 KB per env (Small / Large: observe -5 % / -2 %, Large-16's sampler route -3 %,
+// Small-4's 1-step sampler -3 %), except in multi-step sampler fragments (Small-4 +11 %); plain for
+// Medium's rows (nontemporal: observe +10 %, sampler step +24 %).  The fragment operand plain: stored
+// nontemporal it is written 5-11 % faster but the policy network then reads it from HBM instead of
+// the last-level cache, and the policy route is 1 % slower at Medium-8 (no gain at Large-16).
+// -DWH_OBS_NT / -DWH_OBS_NO_NT: every single-step row store nontemporal / none (A/B switches).
 template <class C>
 constexpr bool rows_nt() {
 #if defined(WH_OBS_NT)
@@ -90,11 +92,7 @@ constexpr bool rows_nt() {
   return C::NAM * C::L * 4 <= 1024 || C::NAM * C::L * 4 > 4096;
 #endif
 }
-#ifdef WH_OBS_NO_NT
 constexpr bool kFragNT = false;
-#else
-constexpr bool kFragNT = true;
-#endif
 
 #ifndef WH_REV_SPLIT_MAX_NAM   // agent counts up to which the move loop has the no-reverse-key variant
 #define WH_REV_SPLIT_MAX_NAM 9
@@ -2372,10 +2370,10 @@ __device__ __forceinline__ void write_image(const Regs<C>& s, const Lds<C>& L, S
 // to one branch and one lgkmcnt(0) round trip per float, four serial LDS latencies per store.  The
 // gather word of both tables is read beside lim, so a float4 costs two LDS round trips, and RU
 // float4s per lane are in flight together.
-template <class C, int NBUF>
+template <class C, bool NTS, int NBUF>
 __device__ __forceinline__ void write_rows(const SampLds<C, NBUF>& O, int buf, float* __restrict__ rows,
                                            uint32_t nenv, uint32_t qe, int tid) {
-  stream_rows<2 * BT, SampLds<C, NBUF>::IMG, rows_nt<C>()>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
+  stream_rows<2 * BT, SampLds<C, NBUF>::IMG, NTS>(O.lim[buf], O.src[0], O.src[1], &O.img[buf][0][0],
                                              reinterpret_cast<f32x4*>(rows), nenv, qe, tid);
 }
 
@@ -2456,7 +2454,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
         write_image<C>(s, L, O, tid, C::NAM, it & 1);
       }
       if (it > 0 && !(ablate & 256))
-        write_rows<C>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+        write_rows<C, false>(O, (it - 1) & 1, obs + (int64_t)(it - 1) * step_floats + e0 * (int64_t)(4 * qe), nenv, qe, tid);
       __syncthreads();
     }
     if (loaded) store_env<C>(s, L, a.state, a.B, e0, na, tid);
@@ -2467,7 +2465,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
       write_image<C>(s, L, O, tid, C::NAM, 0);
     }
     __syncthreads();
-    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    write_rows<C, rows_nt<C>()>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
     if (stepped) {
       run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
@@ -2475,7 +2473,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
     __syncthreads();
-    write_rows<C>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
+    write_rows<C, rows_nt<C>()>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   }
 }
 
