@@ -107,8 +107,14 @@ def cpu_baseline(variant, n, procs, seconds, detail=""):
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
+    # close + join, not the context manager: Pool.__exit__ terminates the workers with SIGTERM, which a
+    # profiler's signal handler logs as an abort per worker (noise in every fault scan of the log)
+    pool = ctx.Pool(procs)
+    try:
         res = pool.map(cpu_worker, [(variant, n, seconds, 1000 + i) for i in range(procs)])
+    finally:
+        pool.close()
+        pool.join()
     rate = sum(a / s for a, s in res if s > 0)
     return dict(value=rate, unit="agent-steps/s", cores=procs, kind="port",
                 sample=f"one process per host core ({procs}; {detail}) x {seconds:.1f} s, 1 env each, "
@@ -288,29 +294,82 @@ def shard_offset(rank, envs_per_gpu):
     return rank * envs_per_gpu
 
 
-def timed_window(run, sync, world, dist):
-    """The contract's timing window: barrier + device sync on both sides of `run`, then the MAX of
-    the per-rank elapsed times (gloo; nothing on the data path).  Returns seconds."""
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    run()
-    sync()
-    elapsed = time.perf_counter() - t0
+# Lead time of the common start: rank 0 names a start instant this far ahead on the node's monotonic
+# clock and every rank spins until it, so the ranks' windows open within microseconds of each other
+# (a barrier alone releases them tens of microseconds apart -- as long as a short timed window).
+START_LEAD_S = 0.005
+
+
+class WindowTime(float):
+    """Seconds of the union window [earliest start, latest end] over the ranks -- what every rank's
+    shard was processed in, so `units of all ranks / this` is the whole job's rate -- carrying each
+    rank's own window on the node's shared monotonic clock (time.perf_counter is CLOCK_MONOTONIC:
+    one clock for every process on the node)."""
+
+    def __new__(cls, starts, ends):
+        w = float.__new__(cls, max(ends) - min(starts))
+        w.starts, w.ends = list(starts), list(ends)
+        return w
+
+    @property
+    def per_rank(self):
+        return [e - s for s, e in zip(self.starts, self.ends)]
+
+    @property
+    def overlap(self):
+        """Fraction of the union window in which every rank's window was open."""
+        common = min(self.ends) - max(self.starts)
+        return max(0.0, common) / float(self) if float(self) > 0 else 1.0
+
+    def describe(self, units_per_rank=None):
+        t0 = min(self.starts)
+        out = {"union_s": float(self), "max_rank_s": max(self.per_rank), "per_rank_s": self.per_rank,
+               "rank_start_offsets_us": [(s - t0) * 1e6 for s in self.starts],
+               "rank_end_offsets_us": [(e - t0) * 1e6 for e in self.ends],
+               "overlap_frac": self.overlap,
+               "note": "value = units of all ranks / union_s (the union of the ranks' windows on the node's "
+                       "monotonic clock); per_rank_s are the ranks' own windows, overlap_frac the share of "
+                       "the union in which all of them were open"}
+        if units_per_rank is not None:
+            out["per_rank_rate"] = [units_per_rank / w for w in self.per_rank]
+        return out
+
+
+def timed_window(run, sync, world, dist, start_delay=0.0):
+    """The contract's timing window: barrier + device sync on both sides of `run`, all ranks starting
+    at a common instant (rank 0 broadcasts it; START_LEAD_S ahead), each rank's [start, end] taken on
+    the node's shared monotonic clock and gathered (gloo; nothing on the data path).  Returns a
+    WindowTime: the union window, >= the slowest rank's own window (the contract's max over ranks).
+    start_delay: seconds this rank waits past the common start (tests: deliberately skewed ranks)."""
     if world > 1:
         import torch
 
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
+    sync()
+    if world > 1:
+        at = torch.tensor([time.perf_counter() + START_LEAD_S], dtype=torch.float64)
+        dist.broadcast(at, src=0)
+        start_at = float(at.item())
+        while time.perf_counter() < start_at:
+            pass
+    if start_delay:
+        time.sleep(start_delay)
+    t0 = time.perf_counter()
+    run()
+    sync()
+    t1 = time.perf_counter()
+    if world == 1:
+        return WindowTime([t0], [t1])
+    dist.barrier()
+    mine = torch.tensor([t0, t1], dtype=torch.float64)
+    allw = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allw, mine)
+    return WindowTime([float(w[0]) for w in allw], [float(w[1]) for w in allw])
 
 
 def aggregate_rate(world, envs_per_gpu, agents, steps, elapsed):
     """Whole-job agent-steps/s: every rank stepped its B envs x agents for `steps` steps inside the
-    window whose length is the slowest rank's."""
+    union of the ranks' windows (timed_window)."""
     return world * envs_per_gpu * agents * steps / elapsed
 
 
@@ -405,7 +464,8 @@ def measure(env, mode, policy, K, W, chunk, dev, world, dist, position=True):
     bytes_total = sum(B * (2 * 4 * env.layout.words_per_env + c * (4 * NA + 1)) for c in plan)
     dones = int(dn.sum().item()) if (dn is not None and whole) else None
     start = (pre + setup + W) % T
-    return dict(elapsed=elapsed, span_ms=span_ms, kernel_ms=span_ms / kernels, launches=kernels,
+    return dict(elapsed=elapsed, window=elapsed.describe(B * NA * K), span_ms=span_ms, kernel_ms=span_ms / kernels,
+                launches=kernels,
                 steps_per_launch=plan[0], bytes_per_launch=bytes_total / kernels,
                 achieved_gbs=bytes_total / (span_ms * 1e-3) / 1e9, bytes_per_env_step=bytes_total / (B * K),
                 host_fixed_us=(elapsed * 1e3 - span_ms) * 1e3, setup_steps=pre + setup,
@@ -462,8 +522,38 @@ def measure_sampler(env, K, W, dev, world, dist):
              "step_only": per_launch(lambda: env.sampler_step("greedy", 0.0, observe=False)),
              "observe_only": per_launch(env.observe),
              "write_ceiling": per_launch(lambda: rows.fill_(1.0))}
-    del rows
+    # The env-owned rows are rewritten in place every step (the sampler API's buffer), so at Medium-8
+    # (172 MB) they stay in the 256 MB last-level cache (MALL).  The same launches writing a ring of
+    # ROT buffers (> 600 MB: fresh HBM every step), and the fill_ of that ring, are the HBM figures.
+    ROT = 4
+    ring = [torch.empty_like(rows) for _ in range(ROT)]
+    own = env._obs
+    state = {"i": 0}
+
+    def one_rot():
+        env._obs = ring[state["i"] % ROT]
+        state["i"] += 1
+        env.sampler_step("greedy", 0.0, observe=True)
+
+    def fill_rot():
+        ring[state["i"] % ROT].fill_(1.0)
+        state["i"] += 1
+
+    split["sampler_step_rotating"] = per_launch(one_rot)
+    split["write_ceiling_rotating"] = per_launch(fill_rot)
+    env._obs = own
+    del rows, ring
+    split["rotating_buffers"] = ROT
     return elapsed, split
+
+
+def sampler_fused(env):
+    """Whether wh_sampler_step runs as one k_sampler launch for env's shape (warehouse_amd.hip
+    wh_sampler_step: the fast step instance -- every slot live, even agent count -- and at most 4 KB of
+    rows per env, fuse_rows), else the step launch + k_observe."""
+    NA = env.agent_slots
+    return (NA % 2 == 0 and env.layout.kernel_agents == NA and not env.train
+            and 4 * NA * env.obs_len <= 4096)
 
 
 def sampler_line(env, Ks, el, split, world, variant, words, fused):
@@ -478,7 +568,7 @@ def sampler_line(env, Ks, el, split, world, variant, words, fused):
     # the two-launch form: the observation launch reads it again) + rewards + dones
     samp_b = rows_b + (2 if fused else 3) * B * 4 * words + B * (4 * NA + 1)
     kname = "k_sampler" if fused else "k_step (1 step) + k_observe"
-    return {
+    out = {
         "workload": f"RLlib sampler route, {variant} N={NA}, B={B}: device greedy policy + step + auto-reset + f32 "
                     f"observation rows [B,{NA},{env.obs_len}] per step (wh_sampler_step -> "
                     f"{'one k_sampler launch' if fused else 'k_step + k_observe'}); hipGraph of 100 steps",
@@ -499,10 +589,26 @@ def sampler_line(env, Ks, el, split, world, variant, words, fused):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": samp_b / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "write_ceiling_frac": rows_b / (split["write_ceiling"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "footprint": (f"{rows_b / 1e6:.0f} MB of rows rewritten in place every step (the env-owned "
+                                   f"buffer): " + ("it fits the 256 MB last-level cache (MALL), so `frac` is a "
+                                                   "cache-resident rate, not HBM" if rows_b < 256e6 else
+                                                   "larger than the 256 MB last-level cache: HBM")),
                      "note": "algorithmic bytes = B*NA*(9R+1)*4 rows + packed state (read + write, + a second "
                              "read for the two-launch form) + rewards + dones; write_ceiling_frac = the rows' bytes "
                              "/ the fill_ time / 8 TB/s"},
     }
+    if "sampler_step_rotating" in split:
+        rms, rot = split["sampler_step_rotating"], split["rotating_buffers"]
+        out["roofline_rotating"] = {
+            "bound": "hbm", "kernel": kname, "kernel_ms": rms, "bytes_per_launch": samp_b,
+            "achieved": samp_b / (rms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": samp_b / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "write_ceiling_ms": split["write_ceiling_rotating"],
+            "write_ceiling_frac": rows_b / (split["write_ceiling_rotating"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "vs_write_ceiling": split["write_ceiling_rotating"] / rms,
+            "footprint": f"the same launches writing a ring of {rot} row buffers ({rot * rows_b / 1e6:.0f} MB): every "
+                         "step's rows go to memory the last-level cache does not hold -- the HBM figure"}
+    return out
 
 
 def measure_sampler_rollout(env, K, frag, W, dev, world, dist):
@@ -541,7 +647,7 @@ def measure_sampler_rollout(env, K, frag, W, dev, world, dist):
     return elapsed, n * frag, kms[len(kms) // 2]
 
 
-def measure_vector(env, K, W, dev, world, dist):
+def measure_vector(env, K, W, dev, world, dist, order=None):
     """The RLlib route with the learner's actions (scripts/train.py's MultiAgentEnv sampler, through
     WarehouseVectorEnv): per step wh_vector_step = external actions [B,NA] -> step + auto-reset +
     observation rows, one launch (k_sampler's generic instance).  The actions are one fixed tensor
@@ -553,7 +659,7 @@ def measure_vector(env, K, W, dev, world, dist):
     acts = env.policy("greedy", 0.0).clone()
 
     def one():
-        env.vector_step(acts, autoreset=True)
+        env.vector_step(acts, autoreset=True, order=order)
 
     for _ in range(max(W, 3)):
         one()
@@ -686,13 +792,56 @@ def mlp_kernel_name(net, prec):
     return "k_mlp (v_mfma_f32_32x32x16_bf16)"
 
 
-def step_roofline(m, variant, NA, policy, mode):
+def profile_tag(variant, NA, policy, envs, mode, steps_per_launch):
+    """The profiles/pmc_traffic.json key of a step-kernel launch shape: the C3/C4 greedy shapes at
+    B = 65,536 keep their short keys, other shapes name policy and batch."""
+    if policy == "greedy" and envs == 65536:
+        return f"{variant}_n{NA}_{mode}_k{steps_per_launch}"
+    return f"{variant}_n{NA}_{policy}_b{envs}_{mode}_k{steps_per_launch}"
+
+
+def config_leg(name, variant, NA, B, policy, K, W, chunk, dev, world, dist, rank):
+    """Another BASELINE config through the headline's own measurement (measure(): one prepared launch
+    of K fused steps -- policy + step + auto-reset, rewards and dones written -- timed inside the
+    contract's window, placed across an episode end), with its own roofline."""
+    import warehouse
+
+    env = warehouse.BatchedWarehouse(variant, B, NA, seed=1234, env_offset=shard_offset(rank, B), device=dev)
+    env.reset()
+    m = measure(env, "fused", policy, K, W, chunk, dev, world, dist)
+    return {"workload": f"{name}: {variant} N={NA}, B={B} envs/GPU, {policy} policy fused with step + auto-reset, "
+                        f"{m['launches']} launch(es) of {m['steps_per_launch']} steps",
+            "value": aggregate_rate(world, B, NA, K, m["elapsed"]), "unit": "agent-steps/s", "steps": K,
+            "ms_per_step": m["elapsed"] * 1e3 / K, "window": m["window"],
+            "dones_in_window": m["dones_in_window"],
+            "roofline": step_roofline(m, variant, NA, policy, "fused", B)}
+
+
+def vector_leg(env, K, W, dev, world, dist, label, order=None):
+    """wh_vector_step (external actions, auto-reset, f32 rows) at env's shape: throughput and the
+    HBM roofline of the launch(es) per step."""
+    B, NA = env.B, env.agent_slots
+    el, vms = measure_vector(env, K, W, dev, world, dist, order=order)
+    words = env.layout.words_per_env
+    fused = sampler_fused(env) or (order is not None and 4 * NA * env.obs_len <= 4096 and NA % 2 == 0)
+    vec_b = (B * NA * env.obs_len * 4 + (2 if fused else 3) * B * 4 * words + B * (4 * NA + 1) + B * NA * 4
+             + (0 if order is None else 4 * order.numel()))
+    return {"workload": label, "value": aggregate_rate(world, B, NA, K, el), "unit": "agent-steps/s", "steps": K,
+            "ms_per_step": el * 1e3 / K,
+            "roofline": {"bound": "hbm", "kernel": "k_sampler<external actions>" if fused else "k_step + k_observe",
+                         "kernel_ms": vms, "bytes_per_launch": vec_b, "achieved": vec_b / (vms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": vec_b / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "algorithmic bytes = rows + packed state (read + write, + a second read for two "
+                                 "launches) + rewards + dones + actions (+ order rows)"}}
+
+
+def step_roofline(m, variant, NA, policy, mode, envs=65536):
     """The bench line's `roofline` for the timed launches of measure() (dict m).  achieved / peak /
     frac are the contract's HBM figures (algorithmic bytes per launch / the launch's event-timed
     duration, against 8 TB/s); `valu` is the chip-level VALU issue roofline of the same launch (from
     the same-sha SQ profile), and `bound` names whichever of the two fractions is higher -- the
     step kernel keeps its state in registers and is VALU-issue bound."""
-    tag = f"{variant}_n{NA}_{mode}_k{m['steps_per_launch']}"
+    tag = profile_tag(variant, NA, policy, envs, mode, m["steps_per_launch"])
     prof = load_profile(tag)
     hbm_frac = m["achieved_gbs"] / HBM_PEAK_GBS
     valu = valu_roofline(prof, m["kernel_ms"])
@@ -761,6 +910,7 @@ def plumbing_only(args, world, rank, dist):
                 "value": aggregate_rate(world, B, NA, K, elapsed), "unit": "agent-steps/s", "n_gpus": world,
                 "steps": K, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / K, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none: no kernel ran",
+                "window": elapsed.describe(B * NA * K),
                 "config": {"workload": "plumbing self-test", "envs_per_gpu": B, "agents": NA,
                            "shard_offsets": offsets,
                            "launch": "self-launched ranks" if os.environ.get("WH_BENCH_SELF_LAUNCHED") else
@@ -787,6 +937,7 @@ def main():
     ap.add_argument("--no-sampler", action="store_true", help="skip the sampler-path (obs) measurement")
     ap.add_argument("--no-desync", action="store_true", help="skip the desynchronised-episodes measurement")
     ap.add_argument("--no-policy", action="store_true", help="skip the SAC-policy rollout measurement")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C2 / C4 legs")
     ap.add_argument("--policy-steps", type=int, default=200)
     ap.add_argument("--policy-steps-f32", type=int, default=40)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = one per host core (host_cores())")
@@ -877,7 +1028,7 @@ def main():
         # not one graph launch's host latency over a 20-step window)
         Ks = max(min(K, 1000), 200)
         el3, split = measure_sampler(env, Ks, W, dev, world, dist)
-        sampler = sampler_line(env, Ks, el3, split, world, args.variant, words, fused=True)
+        sampler = sampler_line(env, Ks, el3, split, world, args.variant, words, fused=sampler_fused(env))
         sampler["roofline"]["traffic"] = load_traffic(f"{args.variant}_n{NA}_sampler")
         el5, Kpp = measure_sampler_pipeline(env, Ks, W, dev, world, dist)
         sampler["two_stream_pipeline"] = {
@@ -894,7 +1045,8 @@ def main():
         env4 = warehouse.BatchedWarehouse("large", B, 16, seed=1234, env_offset=shard_offset(rank, B), device=dev)
         env4.reset()
         el8, split8 = measure_sampler(env4, 200, W, dev, world, dist)
-        sampler_c4 = sampler_line(env4, 200, el8, split8, world, "large", env4.layout.words_per_env, fused=False)
+        sampler_c4 = sampler_line(env4, 200, el8, split8, world, "large", env4.layout.words_per_env,
+                                  fused=sampler_fused(env4))
         del env4
 
     fragment = None
@@ -930,6 +1082,36 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": vec_b / (vms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "note": "algorithmic bytes = rows + 2 x packed state + rewards + dones + actions"},
         }
+
+    # BASELINE configs 2 and 4 through the headline's measurement, in the same run (C3 is the headline)
+    legs = {}
+    if not args.no_configs and (args.variant, NA, B, args.policy) == ("medium", 8, 65536, "greedy"):
+        legs["C2"] = config_leg("C2", "small", 4, 4096, "random", K, W, args.chunk, dev, world, dist, rank)
+        legs["C4"] = config_leg("C4", "large", 16, 65536, "greedy", K, W, args.chunk, dev, world, dist, rank)
+
+    # the RLlib route of scripts/train.py's actual env (all three registered names build
+    # WarehouseLargeTrain, scripts/train.py:34-35): external actions, n redrawn at every auto-reset
+    vector_lt = vector_order = None
+    if not args.no_sampler and (args.variant, NA, B) == ("medium", 8, 65536):
+        import torch
+
+        envt = warehouse.BatchedWarehouse("large", B, None, train=True, seed=1234, env_offset=shard_offset(rank, B),
+                                          device=dev)
+        envt.reset()
+        vector_lt = vector_leg(envt, 200, W, dev, world, dist,
+                               f"scripts/train.py's env (WarehouseLargeTrain: 16 agent slots, n ~ U{{1..16}} per "
+                               f"episode), B={B}: wh_vector_step(actions) = step + auto-reset + f32 rows; hipGraph "
+                               f"of 100 steps")
+        del envt
+        # the dict-order kernel (WarehouseBaseEnv with shuffled action dicts): every env's full dict in
+        # a fixed random order
+        g = torch.Generator(device=dev).manual_seed(7)
+        order = torch.argsort(torch.rand((B, NA), device=dev, generator=g), dim=1).to(torch.int32)
+        env.reset()
+        vector_order = vector_leg(env, 200, W, dev, world, dist,
+                                  f"dict-order route (WarehouseBaseEnv.send_actions with shuffled dicts): "
+                                  f"wh_vector_step(actions, order) at {args.variant} N={NA}, B={B}, every env's dict "
+                                  f"in a random order; hipGraph of 100 steps", order=order)
 
     policy_line = policy_f32 = None
     if not args.no_policy:
@@ -992,6 +1174,7 @@ def main():
             "devices": {"physical_devices": ndev, "devices_shared": shared,
                         "launch": "self-launched ranks" if os.environ.get("WH_BENCH_SELF_LAUNCHED") else
                                   ("torch.distributed.run" if world > 1 else "single process")},
+            "window": m["window"],
             "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
             "alt_launch_mode": alt,
             "desync_episodes": desync,
@@ -999,6 +1182,9 @@ def main():
             "sampler_path_c4": sampler_c4,
             "sampler_fragments": fragment,
             "vector_path": vector,
+            "vector_path_large_train": vector_lt,
+            "vector_path_dict_order": vector_order,
+            "config_legs": legs,
             "policy_path": policy_line,
             "policy_path_f32": policy_f32,
         }

@@ -5,7 +5,11 @@
  * `Warehouse.step()` (warehouse/core.py:167-442) and the greedy baseline policy
  * (baseline/solvers.py:27-58), run for B independent episodes on one GPU.  Plain pointers and
  * sizes only; every pointer named "device" is HIP device memory, `stream` is a hipStream_t
- * (NULL = the default stream).  All calls are asynchronous on `stream` except where noted, return
+ * (NULL = the default stream).  The host engine (libwarehouse_host.so, csrc/host_engine.cpp: the
+ * same entry points on host cores, for hosts without a GPU) takes host memory for every "device"
+ * pointer, ignores `stream`, runs synchronously, and returns WH_ENOTSUP for the device-only entry
+ * points (policy network, fragment operand, two-stream and prepared launches, assert mode).
+ * All calls are asynchronous on `stream` except where noted, return
  * WH_OK (0) or a WH_E* code, and never throw.  The reference is Python, so the binding a maintainer
  * adds on the reference side is ctypes; `warehouse/_native.py` is that binding.
  *
@@ -107,18 +111,20 @@ int wh_reset(const wh_config* cfg, int64_t B, uint32_t* state, const uint8_t* ma
 
 /* Warehouse.step(action_dict)  (warehouse/core.py:262-442).
  *   actions   [B,NA] int32 in 0..8 (MOVES index, core.py:38; the host wraps -9..-1 like Python)
- *   order     [B,NA] int32 or NULL: action-dict iteration order (core.py:279), -1 terminated;
- *             agents not listed do not move.  NULL = ascending agent id.  Entry = agent id in
- *             bits 0-7, optionally (bits 8-15) that dict entry's own action + 1, 0 = actions[e,id]:
- *             a dict naming one agent under two keys ('0' and 0, or '-1' and str(n-1): int(key)
+ *   order     [B,OL] int32 or NULL: action-dict iteration order (core.py:279), -1 entries skipped
+ *             (rows are -1 padded); agents not listed do not move.  NULL = ascending agent id.
+ *             Entry = agent id in bits 0-7, optionally (bits 8-15) that dict entry's own action + 1,
+ *             0 = actions[e,id]: a dict naming one agent under several keys ('0', 0, '-n', -n: int(key)
  *             indexes like numpy, core.py:280) moves it once per entry with that entry's action.
+ *   order_len OL, the order row length: 0 = NA, else 1 .. 4*NA (a dict may name every agent under
+ *             all four of its key forms); anything else is WH_EINVAL.
  *   rewards   [B,NA] float32 (core.py:334-368), dones [B] uint8 (core.py:438); either may be NULL
  *   regen     [B,2R] int32 or NULL (philox): R positions into the ascending list of inactive
  *             pickups (the index np.random.choice(inactive,k) picked), then R delivery targets;
  *             only the first k = R - P + |inactive| of each are read.
  *   n_inactive [B] int32 or NULL: |inactive| before regeneration (core.py:338). */
 int wh_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-            const int32_t* order, float* rewards, uint8_t* dones, const int32_t* regen,
+            const int32_t* order, int32_t order_len, float* rewards, uint8_t* dones, const int32_t* regen,
             int32_t* n_inactive, int32_t phase, uint64_t seed, int64_t env_offset, void* stream);
 
 /* Per-agent observation rows (core.py:224-260 after reset, 371-432 after a step, including the
@@ -173,15 +179,16 @@ int wh_rollout(const wh_config* cfg, int64_t B, uint32_t* state, int32_t steps, 
  * (variable_n != 0) redraw n there, variants.py:69-71 -- then wh_observe into obs (NULL = skip).
  * With autoreset the obs rows of a done env are the first rows of its next episode.
  *   actions [B,NA] int32 0..8 (others act as 4 = stay)
- *   order   [B,NA] int32 or NULL: each env's action-dict iteration order (core.py:279), -1
- *           terminated; agents not listed are skipped -- they neither move nor re-mark their cell
- *           (core.py:279-300 only visits the dict's keys).  NULL = every agent, ascending id.
- *           Entries as wh_step's (bits 8-15: the entry's own action + 1, for repeated agents).
+ *   order   [B,OL] int32 or NULL (OL = order_len as in wh_step): each env's action-dict iteration
+ *           order (core.py:279), -1 padded; agents not listed are skipped -- they neither move nor
+ *           re-mark their cell (core.py:279-300 only visits the dict's keys).  NULL = every agent,
+ *           ascending id.  Entries as wh_step's (bits 8-15: the entry's own action + 1, for repeated
+ *           agents).
  *   mask [B] uint8 or NULL: only envs with mask != 0 are stepped (the others keep their state;
  *   their rewards/dones are not written); rewards [B,NA] / dones [B] / obs [B,NA,9R+1] / stats
  *   may be NULL. */
 int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                   const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
+                   const int32_t* order, int32_t order_len, const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
                    const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream);
 
@@ -191,7 +198,7 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
  * operand).  The same transitions and operand bytes as wh_vector_step(obs = NULL) followed by
  * wh_observe_x (which is what it runs). */
 int wh_vector_step_x(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                     const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, void* xfrag,
+                     const int32_t* order, int32_t order_len, const uint8_t* mask, float* rewards, uint8_t* dones, void* xfrag,
                      const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                      uint64_t seed, int64_t env_offset, void* stream);
 
@@ -239,8 +246,10 @@ int wh_launch_run(const wh_launch* launch);
 int wh_launch_run_timed(const wh_launch* launch, void* start_event, void* stop_event);
 /* Frees a handle of wh_rollout_prepare.  Handles are tracked: run / run_timed / free of a pointer that
  * is not a live handle (never prepared, or already freed) return WH_EINVAL and touch nothing, so a
- * double free is refused instead of corrupting the heap.  NULL is a no-op (WH_OK).  A prepare with
- * B = 0 needs no device and no tables: its handle launches nothing. */
+ * double free is refused instead of corrupting the heap -- as long as no later wh_rollout_prepare
+ * has been handed the same address: a freed handle whose address the allocator reuses is live again
+ * (it names the new launch), so a stale pointer must not be used after a further prepare.  NULL is
+ * a no-op (WH_OK).  A prepare with B = 0 needs no device and no tables: its handle launches nothing. */
 int wh_launch_free(wh_launch* launch);
 
 /* SAC policy network forward (the policy_model of scripts/experiments/warehouse-{small,medium,large}-sac: a

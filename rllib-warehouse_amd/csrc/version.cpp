@@ -19,7 +19,14 @@
 #define WH_MODE ""
 #endif
 
+// The host engine (host_engine.cpp, libwarehouse_host.so) names itself apart from the gfx950 library.
+#ifdef WH_HOST_ENGINE
+#define WH_LIB_NAME "warehouse_host cpu host-engine v1 "
+#else
+#define WH_LIB_NAME "warehouse_amd gfx950 lane-per-env v3 "
+#endif
+
 extern "C" const char* wh_version(void) {
-  return sizeof(WH_VARIANT) > 1 ? "warehouse_amd gfx950 lane-per-env v3 " WH_MODE "sha=" WH_SOURCE_SHA " variant=" WH_VARIANT
-                                : "warehouse_amd gfx950 lane-per-env v3 " WH_MODE "sha=" WH_SOURCE_SHA;
+  return sizeof(WH_VARIANT) > 1 ? WH_LIB_NAME WH_MODE "sha=" WH_SOURCE_SHA " variant=" WH_VARIANT
+                                : WH_LIB_NAME WH_MODE "sha=" WH_SOURCE_SHA;
 }

@@ -917,9 +917,22 @@ struct LazyGrid {
 __device__ unsigned long long g_wh_revcount[2];   // [0] reverse-key loops, [1] crossing-only loops
 #endif
 
+// The action-dict order of the ORDERED path: entry rows [B, ol] (ol = 1 .. 4 * NA: a dict may name an
+// agent under each of its key forms) and the per-lane LDS key list of the entries' moves (16 bits
+// each, [entry][lane]: OKeys, only in the ORDERED instances).
+struct OrderIn {
+  const int32_t* __restrict__ order;
+  int ol;
+  uint16_t* keys;
+};
+template <class C>
+struct OKeys {
+  uint16_t k[4 * C::NAM][BT];
+};
+
 template <class C, bool ORDERED, bool INJ = true, bool CLAMP = true, bool LAZY = false>
 __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (&dstep)[C::NAM],
-                                         const int32_t* __restrict__ order,
+                                         const OrderIn& oi,
                                          const int32_t* __restrict__ actions_g,
                                          const int32_t* __restrict__ regen, const Keys& k,
                                          uint32_t gid, int64_t e, int na, int phase, uint32_t T,
@@ -1014,8 +1027,9 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
     // no pickup point; min3 of the three 0/1-ish terms is 1 exactly when all hold.  Every agent
     // decides against the pre-pickup table (two agents on one point both take it), so the
     // points are cleared only after every agent's target byte has been read (clr[i]: the byte to
-    // zero, row P = scratch).  The ascending move loop decides each agent three turns after its
-    // move, when its lookups have landed, so only a few agents' lookups are live at a time.
+    // zero, row P = scratch).  The ascending move loop issues an agent's three dependent lookups
+    // kPickDist turns apart and decides its pickup 3 * kPickDist turns after its move, when the
+    // last lookup has landed, so only a few agents' lookups are live at a time.
     uint32_t prlo = 0, prhi = 0;   // points picked up, rotated left by one (see pick)
     uint32_t clr[C::NAM];
     auto pick = [&](int i, uint32_t cpv, uint32_t tbv, uint32_t dstv) {
@@ -1089,17 +1103,23 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
         lg->cm = cm;
         lg->rebuild = false;
       }
-      // forbidden (from, to) pairs of accepted moves, key = from | to << 8 (core.py:293-297)
-      uint32_t kk[3 * C::NAM];   // ORDERED path: 3 ordered keys per accepted move
       uint32_t rk[C::NAM], xk[C::NAM];   // ascending path: reverse key, crossing pair
-      if (ORDERED) {   // drop-in single env: agents in action-dict order, records in LDS
+      if (ORDERED) {   // drop-in single env / BaseEnv: entries in action-dict order, records in LDS
+        // Forbidden moves (core.py:293-297) by the one-key-per-move form of the ascending loop (UKEY,
+        // below): a move p -> c is keyed by its direction and its undirected edge / square / cell
+        // (u = p + c per coordinate), and an accepted move forbids exactly the moves with its u and
+        // another direction (an accepted stay: every later stay on its cell, via a flipped low bit).
+        // 16 bits per key: (dx + 1) | (dy + 1) << 2 | xsum << 4 | ysum << 10, so entry k is blocked iff
+        // 1 <= (K_k ^ S_j) <= 15 for an earlier entry j; a rejected entry stores 0xFFFF (xsum 63:
+        // never a real sum, D <= 32).  The keys live in LDS ([entry][lane]), so a dict of any length
+        // up to 4 * NA entries runs in one pass: the first NAM entries unrolled (their order words
+        // and key reads issued together), the rest -- only a dict naming agents under several keys
+        // has them -- in a rolled loop.
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) L.agl[i][tid] = s.ag[i];
-#pragma unroll
-        for (int sidx = 0; sidx < C::NAM; ++sidx) {
-          // entry: agent id in bits 0-7, optionally the slot's own action + 1 in bits 8-15 (a dict
-          // naming one agent under two keys moves it once per key, with that key's action)
-          const int32_t raw = (sidx < na) ? order[e * na + sidx] : -1;
+        auto entry = [&](int sidx, int32_t raw, bool unrolled) {
+          // entry: agent id in bits 0-7, optionally the entry's own action + 1 in bits 8-15 (a dict
+          // naming one agent under several keys moves it once per key, with that key's action)
           int who = raw < 0 ? -1 : (raw & 0xFF);
           const uint32_t sact = raw < 0 ? 0u : ((uint32_t)raw >> 8) & 0xFFu;
           const bool live = who >= 0 && who < (int)n && who < C::NAM;
@@ -1109,21 +1129,30 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           const uint32_t p = a & XY16;
           const uint32_t c = step16<C::D>(p, L.mv(mv > 8u ? 4u : mv));
           const bool occupied = (L.occ[c >> 16][tid] >> (c & 31u)) & 1u;
-          const uint32_t key = p | (c << 8);
-          uint32_t f = 0xFFFFFFFFu;
+          const uint32_t sum = as_u(as_s2(p) + as_s2(c)), dd = pk_sub_i16(c, p);
+          const uint32_t key = (((dd + 1u) & 3u) | ((((dd >> 16) + 1u) & 3u) << 2) | ((sum & 63u) << 4) |
+                                (((sum >> 16) & 63u) << 10));
+          uint32_t f = 15u;
+          if (unrolled) {
 #pragma unroll
-          for (int j = 0; j < 3 * sidx; ++j) f = min(f, kk[j] ^ key);
-          const bool ok = live && !occupied && f != 0u;
+            for (int j = 0; j < C::NAM; ++j)
+              if (j < sidx) f = min(f, (key ^ (uint32_t)oi.keys[j * BT + tid]) - 1u);
+          } else {
+            for (int j = 0; j < sidx; ++j) f = min(f, (key ^ (uint32_t)oi.keys[j * BT + tid]) - 1u);
+          }
+          const bool ok = live && !occupied && f >= 15u;
           atomicAnd(&L.occ[p >> 16][tid], ok ? ~(1u << (p & 31u)) : 0xFFFFFFFFu);
           atomicOr(&L.occ[c >> 16][tid], ok ? (1u << (c & 31u)) : 0u);
-          const uint32_t c1 = (c & 0xFFFFu) | (p & 0xFFFF0000u), c2 = (p & 0xFFFFu) | (c & 0xFFFF0000u);
-          const uint32_t dxy = c ^ p;
-          const bool diag = ok && (dxy & 0xFFFFu) && (dxy >> 16);
-          kk[3 * sidx] = ok ? (c | (p << 8)) : 0xFFFFFFFFu;
-          kk[3 * sidx + 1] = diag ? (c1 | (c2 << 8)) : 0xFFFFFFFFu;
-          kk[3 * sidx + 2] = diag ? (c2 | (c1 << 8)) : 0xFFFFFFFFu;
+          oi.keys[sidx * BT + tid] = (uint16_t)(ok ? (dd == 0u ? key ^ 1u : key) : 0xFFFFu);
           L.agl[who][tid] = ok ? ((a & ~XY16) | c) : a;
-        }
+        };
+        const int32_t* orow = oi.order + e * oi.ol;
+        int32_t raws[C::NAM];
+#pragma unroll
+        for (int sidx = 0; sidx < C::NAM; ++sidx) raws[sidx] = sidx < oi.ol ? orow[sidx] : -1;
+#pragma unroll
+        for (int sidx = 0; sidx < C::NAM; ++sidx) entry(sidx, raws[sidx], true);
+        for (int sidx = C::NAM; sidx < oi.ol; ++sidx) entry(sidx, orow[sidx], false);
 #pragma unroll
         for (int i = 0; i < C::NAM; ++i) s.ag[i] = L.agl[i][tid];
       } else {
@@ -1573,6 +1602,7 @@ struct StepParams {
   const uint32_t* tables;
   const int32_t* actions;
   const int32_t* order;
+  int32_t ol;               // order row length (1 .. 4 * NA; resolve_step turns 0 into NA)
   float* rewards;
   uint8_t* dones;
   float* returns;
@@ -1627,8 +1657,9 @@ __device__ __forceinline__ void flush_episodes(bool fin, uint32_t n, uint32_t re
 // ablation (tools/ablate.py) exists only in builds with -DWH_ABLATION.
 template <class C, int POLICY, bool ORDERED, int PHASE>
 __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C>& L, const Keys& k,
-                                          uint32_t gid, int64_t e, int tid) {
+                                          uint32_t gid, int64_t e, int tid, uint16_t* okeys = nullptr) {
   const int phase = PHASE >= 0 ? PHASE : a.phase;
+  const OrderIn oi{a.order, a.ol, okeys};
 #ifdef WH_ABLATION
   const int ablate = a.ablate;
 #else
@@ -1653,7 +1684,7 @@ __device__ __forceinline__ void run_steps(const StepParams& a, Regs<C>& s, Lds<C
       policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C, ORDERED, true, POLICY != POL_GREEDY || kAblationBuild>(s, L, d, a.order, a.actions, a.regen, k, gid, e, a.na, phase,
+    const bool done = step_env<C, ORDERED, true, POLICY != POL_GREEDY || kAblationBuild>(s, L, d, oi, a.actions, a.regen, k, gid, e, a.na, phase,
                                   (uint32_t)a.T, (uint32_t)a.W, rew, a.n_inactive, tid, ablate);
     if (phase != PH_REGEN) {
       if (a.rewards && !(ablate & 64))
@@ -1766,7 +1797,7 @@ struct FastRun {
       policy_steps<C, POLICY, POLICY == POL_GREEDY && !kAblationBuild>(s, L, k, gid, a.p, d);
     }
     float rew[C::NAM];
-    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, OrderIn{nullptr, 0, nullptr}, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
                                                 (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg);
     if (!(ablate & 64)) {
       store_row<C>(rrow, rew);
@@ -1846,7 +1877,7 @@ __device__ __forceinline__ void run_steps_fast(const StepParams& a, Regs<C>& s, 
       asm volatile("" : "+v"(rb.x), "+v"(rb.y), "+v"(rb.z), "+v"(rb.w));
     }
     float rew[C::NAM];
-    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, nullptr, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
+    const bool done = step_env<C, false, false, POLICY != POL_GREEDY || kAblationBuild, kLazyGrid>(s, L, d, OrderIn{nullptr, 0, nullptr}, nullptr, nullptr, k, gid, e, C::NAM, PH_ALL,
                                                 (uint32_t)a.T, (uint32_t)a.W, rew, nullptr, tid, ablate, &lg,
                                                 kHoistPolicy ? &rb : nullptr);
     if (!(ablate & 64)) {
@@ -1913,6 +1944,7 @@ template <class C, int POLICY, bool ORDERED, bool FAST>
 __global__ __launch_bounds__(BT) void k_step(StepParams a) {
   __shared__ Lds<C> L;
   __shared__ std::conditional_t<FAST, Slots<C>, NoSlots> RS;   // reset slots: fused rollout only
+  __shared__ std::conditional_t<ORDERED, OKeys<C>, NoSlots> OK;   // dict-order move keys: ORDERED only
   const int tid = threadIdx.x;
   if (FAST) WH_T(0);
   const int64_t e = (int64_t)blockIdx.x * BT + tid;
@@ -1964,6 +1996,8 @@ __global__ __launch_bounds__(BT) void k_step(StepParams a) {
     run_steps_fast<C, POLICY>(a, s, L, &RS, k, gid, e, tid);
   else if (!ORDERED && a.phase == PH_ALL)
     run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+  else if constexpr (ORDERED)
+    run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid, &OK.k[0][0]);
   else
     run_steps<C, POLICY, ORDERED, -1>(a, s, L, k, gid, e, tid);
   if (FAST) WH_T(3);
@@ -2094,12 +2128,16 @@ __device__ __forceinline__ void stream_frags(const uint32_t* lims, const uint32_
                                              uint32_t nenv, int na, int tid) {
   constexpr int KQ = (L + 2 + 15) / 16;
   const uint32_t rows = nenv * (uint32_t)na, tiles = (rows + 31u) / 32u;   // (a tail group: fewer)
-  const uint32_t magic = 0xFFFFFFFFu / (uint32_t)na + 1u;   // row / na == umulhi(row, magic) (row * na < 2^32)
+  // row / na == umulhi(row, magic) while row * na < 2^32, for na >= 2; for na == 1 the constant
+  // 2^32 wraps to 0, so that case takes the row itself (every env but the first of a
+  // group read env 0's image)
+  const bool one = na == 1;
+  const uint32_t magic = one ? 0u : 0xFFFFFFFFu / (uint32_t)na + 1u;
   uint4* out = xfrag + ((e0 * na) / 32) * (int64_t)(KQ * 64);
   for (uint32_t c = tid; c < tiles * KQ * 64; c += NT) {
     const uint32_t lane = c & 63u, tq = c >> 6, q = tq % KQ, t = tq / KQ;
     const uint32_t row = t * 32u + (lane & 31u);   // counted from the group's first env
-    const uint32_t el1 = __umulhi(row, magic), i = row - el1 * (uint32_t)na;
+    const uint32_t el1 = one ? row : __umulhi(row, magic), i = row - el1 * (uint32_t)na;
     const bool rl = row < rows;
     const uint32_t lim = lims[rl ? el1 : 0];
     const bool live_row = rl && i < ((lim & 0x7FFFFFFFu) / L);
@@ -2393,6 +2431,7 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
   __shared__ Lds<C> L;
   __shared__ SampLds<C, MULTI ? 2 : 1> O;
   __shared__ std::conditional_t<MULTI, Slots<C>, NoSlots> RS;   // reset slots: multi-step launches
+  __shared__ std::conditional_t<ORDERED, OKeys<C>, NoSlots> OK;   // dict-order move keys: ORDERED only
   const int tid = threadIdx.x;
   const bool stepper = tid < BT;
   const int64_t e0 = (int64_t)blockIdx.x * BT;
@@ -2468,7 +2507,10 @@ __global__ __launch_bounds__(2 * BT) void k_sampler(StepParams a, float* __restr
     write_rows<C, rows_nt<C>()>(O, 0, obs + e0 * (int64_t)(4 * qe), nenv, qe, tid);
   } else {
     if (stepped) {
-      run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
+      if constexpr (ORDERED)
+        run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid, &OK.k[0][0]);
+      else
+        run_steps<C, POLICY, ORDERED, PH_ALL>(a, s, L, k, gid, e, tid);
       store_env<C>(s, L, a.state, a.B, e0, na, tid);
     }
     if (loaded) write_image<C>(s, L, O, tid, na, 0);
@@ -2735,7 +2777,11 @@ Kernels make_kernels() {
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
   k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
-  k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
+  // the dict-order instance also holds the entries' move keys (OKeys: 4 * NAM x 512 bytes)
+  if constexpr (sizeof(Lds<C>) + sizeof(SampLds<C, 1>) + sizeof(OKeys<C>) <= 160 * 1024)
+    k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
+  else
+    k.vsampler[1] = nullptr;
   k.reset = k_reset<C>;
   k.observe[0] = k_observe<C, kObsEB[0]>;
   k.observe[1] = k_observe<C, kObsEB[1]>;
@@ -2958,10 +3004,16 @@ static int resolve_step(const wh_config* cfg, int64_t B, uint32_t* state, int po
   Geometry g;
   const Kernels* k;
   const uint32_t* tab;
-  int rc = prepare(cfg, B, stream, &g, &k, &tab);
+  // host-side argument checks first (no device needed to refuse them)
+  int rc = validate(cfg, &g);
   if (rc) return rc;
   if (policy < 0 || policy > 2) return WH_EINVAL;
   if (B > 0 && !state) return WH_EINVAL;
+  // order rows: 0 = NA entries, else 1 .. 4 * NA (every key form of every agent, core.py:280)
+  if (a.ol == 0) a.ol = g.NA;
+  if (a.ol < 1 || a.ol > 4 * g.NA) return WH_EINVAL;
+  rc = prepare(cfg, B, stream, &g, &k, &tab);
+  if (rc) return rc;
   a.state = state;
   a.B = B;
   a.na = g.NA;
@@ -3002,13 +3054,14 @@ static int launch_step(const wh_config* cfg, int64_t B, uint32_t* state, int pol
 extern "C" {
 
 int wh_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-            const int32_t* order, float* rewards, uint8_t* dones, const int32_t* regen,
+            const int32_t* order, int32_t order_len, float* rewards, uint8_t* dones, const int32_t* regen,
             int32_t* n_inactive, int32_t phase, uint64_t seed, int64_t env_offset, void* stream) {
   if (phase < WH_PHASE_ALL || phase > WH_PHASE_REGEN) return WH_EINVAL;
   if (B > 0 && phase != WH_PHASE_REGEN && !actions) return WH_EINVAL;
   StepParams a{};
   a.actions = actions;
   a.order = order;
+  a.ol = order_len;
   a.rewards = rewards;
   a.dones = dones;
   a.regen = regen;
@@ -3155,14 +3208,15 @@ int wh_observe_x(const wh_config* cfg, int64_t B, const uint32_t* state, float* 
 }
 
 int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                   const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, float* obs,
-                   const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
+                   const int32_t* order, int32_t order_len, const uint8_t* mask, float* rewards, uint8_t* dones,
+                   float* obs, const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                    uint64_t seed, int64_t env_offset, void* stream) {
   if (B > 0 && !actions) return WH_EINVAL;
   if (!stats_ok(stats)) return WH_EINVAL;
   StepParams a{};
   a.actions = actions;
   a.order = order;   // non-NULL: the action-dict order path (k_step<..., ORDERED>), as wh_step
+  a.ol = order_len;
   a.mask = mask;
   a.rewards = rewards;
   a.dones = dones;
@@ -3187,7 +3241,7 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
     // the fast instance when the step resolved to it (every env stepped in ascending order, no
     // metrics, auto-reset: RLlib's common case), else the generic one
     void (*fk)(StepParams, float*) = (l.kern == k->step_fast[0] && k->sampler[0]) ? k->sampler[0] : k->vsampler[order ? 1 : 0];
-    if (fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
+    if (fk && fused_ok(fk) && (g.NA * (9 * g.R + 1)) % 4 == 0 && (uintptr_t)obs % 16 == 0) {
       hipLaunchKernelGGL(fk, grid_for(B), dim3(2 * BT), 0, l.stream, l.a, obs);
       return hip_err(hipGetLastError());
     }
@@ -3203,14 +3257,15 @@ int wh_vector_step(const wh_config* cfg, int64_t B, uint32_t* state, const int32
 // launches, profiles/r05_vsx_ab.txt: the operand's per-byte gathers at 8 waves per CU against
 // k_observe's full occupancy.)
 int wh_vector_step_x(const wh_config* cfg, int64_t B, uint32_t* state, const int32_t* actions,
-                     const int32_t* order, const uint8_t* mask, float* rewards, uint8_t* dones, void* xfrag,
-                     const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
+                     const int32_t* order, int32_t order_len, const uint8_t* mask, float* rewards, uint8_t* dones,
+                     void* xfrag, const wh_episode_stats* stats, int32_t autoreset, int32_t variable_n,
                      uint64_t seed, int64_t env_offset, void* stream) {
   if (B > 0 && (!actions || !xfrag)) return WH_EINVAL;
   if ((uintptr_t)xfrag % 16 != 0 || !stats_ok(stats)) return WH_EINVAL;
   StepParams a{};
   a.actions = actions;
   a.order = order;
+  a.ol = order_len;
   a.mask = mask;
   a.rewards = rewards;
   a.dones = dones;

@@ -1,8 +1,13 @@
-"""ctypes binding of the C ABI in include/warehouse_amd.h (libwarehouse_amd.so, built in-tree).
+"""ctypes binding of the C ABI in include/warehouse_amd.h, built in-tree for two engines:
 
-There is no CPU fallback: if the library or a HIP device is missing, every entry point raises.
-torch is imported first so the library resolves `libamdhip64.so.7` to the HIP runtime torch has
-already loaded (one runtime per process; torch owns device memory and streams).
+  lib()       libwarehouse_amd.so   the gfx950 kernels (device memory, HIP streams)
+  host_lib()  libwarehouse_host.so  the same entry points on host cores (csrc/host_engine.cpp, g++):
+                                    BASELINE config 1 on a host without a GPU
+
+Neither falls back to the other: a missing library raises, and a GPU run never touches the host
+engine (batched.py picks the engine from the device a BatchedWarehouse lives on).  torch is imported
+first so the HIP library resolves `libamdhip64.so.7` to the HIP runtime torch has already loaded
+(one runtime per process; torch owns device memory and streams).
 """
 from __future__ import annotations
 
@@ -16,6 +21,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libwarehouse_amd.so")
 # kernel A/B experiments (tools/ab.sh) point this at an alternative build of the same library
 LIB_PATH = os.environ.get("WAREHOUSE_AMD_LIB", LIB_PATH)
+HOST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libwarehouse_host.so")
 
 WH_OK = 0
 WH_EINVAL = 22
@@ -93,6 +99,7 @@ class WarehouseNativeError(RuntimeError):
 
 
 _lib: Optional[ctypes.CDLL] = None
+_host_lib: Optional[ctypes.CDLL] = None
 
 _P = ctypes.c_void_p
 _I32, _I64, _U64, _F32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
@@ -102,19 +109,31 @@ _CFG = ctypes.POINTER(WhConfig)
 def lib() -> ctypes.CDLL:
     """Load the HIP library (once).  Raises loudly if it has not been built."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+    if _lib is None:
+        _lib = _load(LIB_PATH, os.environ.get("WAREHOUSE_AMD_AB") == "1")
+    return _lib
+
+
+def host_lib() -> ctypes.CDLL:
+    """Load the host engine (once).  Raises loudly if it has not been built."""
+    global _host_lib
+    if _host_lib is None:
+        _host_lib = _load(HOST_LIB_PATH, False)
+    return _host_lib
+
+
+def _load(path: str, ab: bool) -> ctypes.CDLL:
+    if not os.path.exists(path):
         raise WarehouseNativeError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
-            "or `make -C rllib-warehouse_amd/csrc` (there is no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C rllib-warehouse_amd/csrc`")
+    L = ctypes.CDLL(path)
     # Every entry point of include/warehouse_amd.h must be there: argtypes applied to an older build
     # whose signatures differ would turn a missing argument into out-of-bounds device writes.  Only
     # explicit A/B experiments (WAREHOUSE_AMD_AB=1, tools/ab.sh) may load a library lacking some.
     missing = [s for s in SYMBOLS if not hasattr(L, s)]
-    if missing and os.environ.get("WAREHOUSE_AMD_AB") != "1":
-        raise WarehouseNativeError(f"{LIB_PATH} lacks entry points {missing}: built from other sources "
+    if missing and not ab:
+        raise WarehouseNativeError(f"{path} lacks entry points {missing}: built from other sources "
                                    "-- rebuild (__graft_entry__.build())")
 
     class _Sigs:   # (A/B builds only) argtypes of a symbol the library lacks go nowhere
@@ -134,14 +153,14 @@ def lib() -> ctypes.CDLL:
     S.wh_pack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
     S.wh_unpack.argtypes = [_CFG, _I64] + [_P] * 9 + [_P]
     S.wh_reset.argtypes = [_CFG, _I64, _P, _P, ctypes.POINTER(WhResetDraws), _I32, _U64, _I64, _P]
-    S.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P]
+    S.wh_step.argtypes = [_CFG, _I64, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _U64, _I64, _P]
     S.wh_observe.argtypes = [_CFG, _I64, _P, _P, _P]
     S.wh_observe_x.argtypes = [_CFG, _I64, _P, _P, _P, _P]
     S.wh_policy.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _U64, _I64, _P]
     _ST = ctypes.POINTER(WhEpisodeStats)
     S.wh_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
-    S.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
-    S.wh_vector_step_x.argtypes = [_CFG, _I64, _P, _P, _P, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    S.wh_vector_step.argtypes = [_CFG, _I64, _P, _P, _P, _I32, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
+    S.wh_vector_step_x.argtypes = [_CFG, _I64, _P, _P, _P, _I32, _P, _P, _P, _P, _ST, _I32, _I32, _U64, _I64, _P]
     S.wh_sampler_step.argtypes = [_CFG, _I64, _P, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]
     S.wh_sampler_step_to.argtypes = [_CFG, _I64, _P, _P, _I32, _F32, _P, _P, _ST, _I32, _U64, _I64, _P]
     S.wh_sampler_rollout.argtypes = [_CFG, _I64, _P, _I32, _I32, _F32, _P, _P, _P, _ST, _I32, _U64, _I64, _P]
@@ -160,7 +179,6 @@ def lib() -> ctypes.CDLL:
     for name in SYMBOLS:
         if name not in ("wh_version", "wh_launch_free") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
-    _lib = L
     return L
 
 
@@ -189,7 +207,7 @@ def tree_source_sha(csrc: str = CSRC, header: str = HEADER) -> str:
     return h.hexdigest()[:16]
 
 
-_VERSION_RE = re.compile(r"lane-per-env v3 (?:\(assert mode\) )?sha=([0-9a-f]{16}|unknown)(?: variant=([^\x00]*))?")
+_VERSION_RE = re.compile(r"(?:lane-per-env v3|host-engine v1) (?:\(assert mode\) )?sha=([0-9a-f]{16}|unknown)(?: variant=([^\x00]*))?")
 
 
 def parse_version(version) -> tuple:
@@ -208,7 +226,7 @@ def version_sha(version: bytes) -> Optional[str]:
 def file_version(path: str) -> tuple:
     """(sha, variant) baked into a built library file, read from its bytes (no load)."""
     with open(path, "rb") as fh:
-        m = re.search(rb"lane-per-env v3 (?:\(assert mode\) )?sha=(?:[0-9a-f]{16}|unknown)(?: variant=[^\x00]*)?",
+        m = re.search(rb"(?:lane-per-env v3|host-engine v1) (?:\(assert mode\) )?sha=(?:[0-9a-f]{16}|unknown)(?: variant=[^\x00]*)?",
                       fh.read())
     return parse_version(m.group(0)) if m else (None, None)
 
@@ -246,6 +264,13 @@ def verify_provenance(extra_libs=()) -> str:
     return want
 
 
+def verify_host_provenance() -> str:
+    """verify_provenance for the host engine: built from this tree's sources, no variant."""
+    want = tree_source_sha()
+    check_provenance(host_lib().wh_version(), want, ("",), HOST_LIB_PATH)
+    return want
+
+
 def check(rc: int, what: str) -> None:
     if rc == WH_OK:
         return
@@ -268,18 +293,19 @@ def make_config(area_dimension, num_requests, racks, agent_slots, episode_durati
                     int(episode_duration), int(pickup_wait_duration))
 
 
-def query(cfg: WhConfig) -> WhLayout:
+def query(cfg: WhConfig, L=None) -> WhLayout:
+    """wh_query of the HIP library (or of the engine L)."""
     out = WhLayout()
-    check(lib().wh_query(ctypes.byref(cfg), ctypes.byref(out)), "wh_query")
+    check((L or lib()).wh_query(ctypes.byref(cfg), ctypes.byref(out)), "wh_query")
     return out
 
 
-def ptr(t) -> Optional[int]:
-    """data pointer of a device tensor (None -> NULL)."""
+def ptr(t, host: bool = False) -> Optional[int]:
+    """data pointer of a device tensor -- a host tensor for the host engine (None -> NULL)."""
     if t is None:
         return None
-    if not t.is_cuda:
-        raise ValueError("warehouse kernels take device tensors")
+    if t.is_cuda == host:
+        raise ValueError("the host engine takes host tensors" if host else "warehouse kernels take device tensors")
     if not t.is_contiguous():
         raise ValueError("warehouse kernels take contiguous tensors")
     return t.data_ptr()
@@ -291,7 +317,9 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 def stream_of(device) -> int:
     """The current HIP stream of `device` as a raw handle: every launch resolves it, so the
     single-env drop-in pays it several times per step -- the raw accessor skips building a
-    torch Stream object (~5 us each)."""
+    torch Stream object (~5 us each).  A host device has none (0)."""
+    if isinstance(device, torch.device) and device.type == "cpu":
+        return 0
     if _raw_stream is not None:
         idx = device.index if isinstance(device, torch.device) and device.index is not None \
             else torch.cuda.current_device()

@@ -1,7 +1,10 @@
-"""B independent warehouse episodes resident on one MI355X.
+"""B independent warehouse episodes resident on one MI355X (or, without a GPU, on host cores).
 
 `BatchedWarehouse` owns the packed struct-of-arrays state (include/warehouse_amd.h, "PACKED
-STATE") as one int32 device tensor `state[words, B]` and drives the HIP kernels through the C ABI:
+STATE") as one int32 tensor `state[words, B]` and drives an engine through the C ABI: the HIP
+kernels (libwarehouse_amd.so) for a batch on a HIP device, the host engine (libwarehouse_host.so,
+csrc/host_engine.cpp) for a batch on "cpu" -- the device the caller names, or the host when no HIP
+device is visible (BASELINE config 1).  Same entry points, state layout and draws either way:
 
     reset()    -> wh_reset    Warehouse.reset()              warehouse/core.py:167-260
     step()     -> wh_step     Warehouse.step()               warehouse/core.py:262-442
@@ -29,10 +32,22 @@ from ._geometry import GEOMETRY
 POLICIES = {"greedy": nat.WH_POLICY_GREEDY, "random": nat.WH_POLICY_RANDOM}
 
 
+def resolve_device(device=None) -> torch.device:
+    """The device a batch lives on: a HIP device (the gfx950 kernels) or the host ("cpu": the host
+    engine).  None = the current HIP device, or the host when no HIP device is visible.  Naming a
+    HIP device on a host without one raises -- nothing silently moves to the host engine."""
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    dev = torch.device(device)
+    if dev.type == "cpu":
+        return dev
+    return require_device(dev)
+
+
 def require_device(device=None) -> torch.device:
     if not torch.cuda.is_available():
-        raise RuntimeError("warehouse: no HIP device visible -- the simulator runs only on an "
-                           "MI355X (gfx950); there is no CPU fallback")
+        raise RuntimeError("warehouse: no HIP device visible -- the gfx950 kernels need an MI355X; there "
+                           "is no CPU fallback (device='cpu' selects the host engine explicitly)")
     dev = torch.device(device if device is not None else "cuda")
     if dev.type != "cuda":
         raise RuntimeError(f"warehouse: device {dev} is not a HIP device")
@@ -54,6 +69,17 @@ def _check_out(t, shape, dtype, device):
     if not t.is_contiguous():
         raise ValueError("warehouse kernels take contiguous tensors")
     return t
+
+
+def _dev_mask(mask, device, B):
+    """An env mask [B] as the uint8 device operand the kernels read (mask[e] for every e < B): any
+    bool/int array or tensor of exactly B entries; another length would be read past its end."""
+    if mask is None:
+        return None
+    m = torch.as_tensor(np.asarray(mask) if not torch.is_tensor(mask) else mask)
+    if tuple(m.shape) != (B,):
+        raise ValueError(f"mask: expected shape ({B},), got {tuple(m.shape)}")
+    return m.to(device=device, dtype=torch.uint8).contiguous()
 
 
 def _dev_i32(x, device, shape=None):
@@ -144,8 +170,10 @@ class BatchedWarehouse:
             raise AssertionError("num_agents <= num_requests (core.py:89)")
         self.agent_slots = slots
         self.cfg = nat.make_config(geo["D"], geo["R"], geo["racks"], slots, geo["T"], geo["W"])
-        self.layout = nat.query(self.cfg)
-        self.device = require_device(device)
+        self.device = resolve_device(device)
+        self.host = self.device.type == "cpu"          # the host engine (no HIP device)
+        self._lib = nat.host_lib() if self.host else nat.lib()
+        self.layout = nat.query(self.cfg, self._lib)
         self.B = int(num_envs)
         self.seed = int(seed)
         self.env_offset = int(env_offset)
@@ -172,15 +200,28 @@ class BatchedWarehouse:
         return nat.stream_of(self.device)
 
     def _call(self, name, *args):
-        nat.check(getattr(nat.lib(), name)(self._cfgp, self.B, *args), name)
+        nat.check(getattr(self._lib, name)(self._cfgp, self.B, *args), name)
+
+    def _ptr(self, t):
+        return nat.ptr(t, self.host)
+
+    def _order(self, order):
+        """An action-dict order operand [B, OL] (OL = 1 .. 4 * agent_slots, -1 padded; see
+        include/warehouse_amd.h wh_step) and its row length, or (None, 0)."""
+        if order is None:
+            return None, 0
+        o = _dev_i32(order, self.device)
+        if o.dim() == 1 and self.B == 1:
+            o = o.reshape(1, -1)
+        if o.dim() != 2 or o.shape[0] != self.B or not 1 <= o.shape[1] <= 4 * self.agent_slots:
+            raise ValueError(f"order: expected shape ({self.B}, 1..{4 * self.agent_slots}), got {tuple(o.shape)}")
+        return o, int(o.shape[1])
 
     # ------------------------------------------------------------------ API
     def reset(self, mask=None, draws: Optional[Dict[str, object]] = None) -> None:
         """Reset the envs selected by `mask` ([B] bool; None = all).  `draws` injects the
         reference's reset draws: spawn [B,NA,2], pickups [B,R], targets [B,R], n [B] (optional)."""
-        m = None
-        if mask is not None:
-            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        m = _dev_mask(mask, self.device, self.B)
         keep = []
         dp = None
         if draws is not None:
@@ -191,7 +232,7 @@ class BatchedWarehouse:
             keep = [sp, pk, tg, nn]
             dp = ctypes.byref(nat.WhResetDraws(sp.data_ptr(), pk.data_ptr(), tg.data_ptr(),
                                                None if nn is None else nn.data_ptr()))
-        self._call("wh_reset", self.state.data_ptr(), nat.ptr(m), dp, int(self.train),
+        self._call("wh_reset", self.state.data_ptr(), self._ptr(m), dp, int(self.train),
                    self.seed, self.env_offset, self.stream)
         if self.stats is not None:   # a reset starts a new episode return
             if m is None:
@@ -202,14 +243,14 @@ class BatchedWarehouse:
 
     def step(self, actions, order=None, regen=None, phase: int = nat.WH_PHASE_ALL
              ) -> Tuple[torch.Tensor, torch.Tensor]:
-        """One transition for every env.  actions [B,NA] in 0..8; order [B,NA] (-1 padded) is the
-        action-dict iteration order; regen [B,2R] injects the regeneration draws.  Returns the
-        env-owned (rewards [B,NA] float32, dones [B] uint8) buffers, overwritten next call."""
+        """One transition for every env.  actions [B,NA] in 0..8; order [B,OL] (OL up to 4 NA, -1
+        padded) is the action-dict iteration order; regen [B,2R] injects the regeneration draws.
+        Returns the env-owned (rewards [B,NA] float32, dones [B] uint8) buffers, overwritten next call."""
         a = None if actions is None else _dev_i32(actions, self.device, (self.B, self.agent_slots))
-        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
+        o, ol = self._order(order)
         r = _dev_i32(regen, self.device, (self.B, 2 * self.R))
-        self._call("wh_step", self.state.data_ptr(), nat.ptr(a), nat.ptr(o), self.rewards.data_ptr(),
-                   self.dones.data_ptr(), nat.ptr(r), self.n_inactive.data_ptr(), int(phase),
+        self._call("wh_step", self.state.data_ptr(), self._ptr(a), self._ptr(o), ol, self.rewards.data_ptr(),
+                   self.dones.data_ptr(), self._ptr(r), self.n_inactive.data_ptr(), int(phase),
                    self.seed, self.env_offset, self.stream)
         return self.rewards, self.dones
 
@@ -251,16 +292,15 @@ class BatchedWarehouse:
         obs rows of a done env already belong to its next episode.  Rewards/dones of envs outside
         `mask` are stale."""
         a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
-        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
-        m = None
-        if mask is not None:
-            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        o, ol = self._order(order)
+        m = _dev_mask(mask, self.device, self.B)
         if observe and self._obs is None:
             self._obs = torch.empty((self.B, self.agent_slots, self.obs_len), dtype=torch.float32,
                                     device=self.device)
         obs = self._obs if observe else None
-        self._call("wh_vector_step", self.state.data_ptr(), a.data_ptr(), nat.ptr(o), nat.ptr(m), self.rewards.data_ptr(),
-                   self.dones.data_ptr(), nat.ptr(obs), None if self.stats is None else self.stats.ref,
+        self._call("wh_vector_step", self.state.data_ptr(), a.data_ptr(), self._ptr(o), ol, self._ptr(m),
+                   self.rewards.data_ptr(), self.dones.data_ptr(), self._ptr(obs),
+                   None if self.stats is None else self.stats.ref,
                    int(bool(autoreset)), int(self.train), self.seed, self.env_offset, self.stream)
         return obs, self.rewards, self.dones
 
@@ -269,12 +309,10 @@ class BatchedWarehouse:
         (wh_vector_step_x: the step, then observe_x()'s buffer).  Returns env-owned
         (fragments [tiles, KQ, 64, 16] uint8, rewards [B,NA], dones [B])."""
         a = _dev_i32(actions, self.device, (self.B, self.agent_slots))
-        o = _dev_i32(order, self.device, (self.B, self.agent_slots))
-        m = None
-        if mask is not None:
-            m = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
+        o, ol = self._order(order)
+        m = _dev_mask(mask, self.device, self.B)
         xf = self._xfrag_buffer()
-        self._call("wh_vector_step_x", self.state.data_ptr(), a.data_ptr(), nat.ptr(o), nat.ptr(m),
+        self._call("wh_vector_step_x", self.state.data_ptr(), a.data_ptr(), self._ptr(o), ol, self._ptr(m),
                    self.rewards.data_ptr(), self.dones.data_ptr(), xf.data_ptr(),
                    None if self.stats is None else self.stats.ref, int(bool(autoreset)), int(self.train),
                    self.seed, self.env_offset, self.stream)
@@ -291,7 +329,7 @@ class BatchedWarehouse:
                                     device=self.device)
         obs = self._obs if observe else None
         self._call("wh_sampler_step", self.state.data_ptr(), POLICIES[policy], float(p),
-                   self.rewards.data_ptr(), self.dones.data_ptr(), nat.ptr(obs),
+                   self.rewards.data_ptr(), self.dones.data_ptr(), self._ptr(obs),
                    None if self.stats is None else self.stats.ref, int(self.train), self.seed,
                    self.env_offset, self.stream)
         return obs, self.rewards, self.dones
@@ -309,7 +347,7 @@ class BatchedWarehouse:
             t = torch.empty(shape, dtype=d, device=self.device) if t is None else _check_out(t, shape, d, self.device)
             out.append(t)
         self._call("wh_sampler_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
-                   nat.ptr(out[1]), nat.ptr(out[2]), nat.ptr(out[0]),
+                   self._ptr(out[1]), self._ptr(out[2]), self._ptr(out[0]),
                    None if self.stats is None else self.stats.ref, int(self.train), self.seed, self.env_offset,
                    self.stream)
         return tuple(out)
@@ -328,7 +366,7 @@ class BatchedWarehouse:
             if t is not None:
                 _check_out(t, shape, d, self.device)
         self._call("wh_rollout", self.state.data_ptr(), int(steps), POLICIES[policy], float(p),
-                   nat.ptr(rewards), nat.ptr(dones), nat.ptr(returns),
+                   self._ptr(rewards), self._ptr(dones), self._ptr(returns),
                    None if self.stats is None else self.stats.ref, int(bool(autoreset)),
                    int(self.train), self.seed, self.env_offset, self.stream)
 
@@ -355,6 +393,9 @@ class BatchedWarehouse:
                             (dones, (steps, self.B), torch.uint8), (returns, (self.B,), torch.float32)):
             if t is not None:
                 _check_out(t, shape, d, self.device)
+        if self.host:
+            raise nat.WarehouseNativeError("rollout_launcher: prepared launches are a device feature "
+                                           "(the host engine runs rollout() directly)")
         lib = nat.lib()
         handle = ctypes.c_void_p()
         nat.check(lib.wh_rollout_prepare(self._cfgp, self.B, self.state.data_ptr(), int(steps), POLICIES[policy],

@@ -2,7 +2,9 @@
 
 Same constructor, attributes and reset()/step() contract as the reference class
 (warehouse/core.py:73-442), so baseline/run.py and scripts/train.py run unchanged.  One env is a
-B=1 batch of `BatchedWarehouse`; every transition runs on the GPU.
+B=1 batch of `BatchedWarehouse`; every transition runs on the GPU -- or, on a host without a HIP
+device, on the host engine (csrc/host_engine.cpp, the same C ABI on host cores: BASELINE config 1,
+"baseline/run.py on CPU").  WAREHOUSE_DEVICE names the device explicitly ("cuda", "cuda:1", "cpu").
 
 RNG parity.  The reference draws from numpy's GLOBAL stream (core.py:196-197, 215-220, 339-350),
 interleaved with whatever else the process draws (e.g. the greedy solver's per-agent coin,
@@ -37,7 +39,7 @@ OBS_KEYS = ("num_agents", "other_availabilities", "other_delivery_targets", "oth
 
 
 def _default_device():
-    return os.environ.get("WAREHOUSE_DEVICE", "cuda")
+    return os.environ.get("WAREHOUSE_DEVICE") or ("cuda" if torch.cuda.is_available() else "cpu")
 
 
 def agent_index(key, n: int) -> int:
@@ -123,11 +125,13 @@ class Warehouse(MultiAgentEnv):
 
     # ------------------------------------------------------------------ helpers
     def _io_buffers(self):
-        """Pinned host and device buffers for the per-step uploads (allocated on first step)."""
+        """Host and device buffers for the per-step uploads (allocated on first step; pinned for a
+        HIP device): io = [actions (n) | dict-order entries (4n)], regen [1, 2R]."""
         if self._io is None:
             n, R, dev = self._num_agents, self._num_requests, self._engine.device
-            h_io = torch.empty((2, n), dtype=torch.int32).pin_memory()
-            h_regen = torch.empty((1, 2 * R), dtype=torch.int32).pin_memory()
+            pin = (lambda t: t) if dev.type == "cpu" else (lambda t: t.pin_memory())
+            h_io = pin(torch.empty((1, 5 * n), dtype=torch.int32))
+            h_regen = pin(torch.empty((1, 2 * R), dtype=torch.int32))
             self._io = (h_io, torch.empty_like(h_io, device=dev), h_regen, torch.empty_like(h_regen, device=dev))
             for entry in self._engine_cache.values():   # kept with the engine for later episodes
                 if entry[0] is self._engine:
@@ -173,24 +177,25 @@ class Warehouse(MultiAgentEnv):
     def step(self, action_dict: Dict[str, int]
              ) -> Tuple[Dict[str, dict], Dict[str, float], Dict[str, bool], Dict[str, dict]]:
         """core.py:262-442 for one env.  Each dict entry moves its agent in iteration order; an agent
-        named under two key forms ('0' and 0, '-1' and str(n - 1)) moves once per entry.
-        Limit (not the reference's): at most `agent_slots` entries per dict -- the kernel's order row
-        is one entry per agent slot -- so a dict naming agents more times than that raises
-        ValueError, where the reference (core.py:279-281) would accept up to 4n key forms."""
+        named under several key forms ('0', 0, '-n', -n: int(key) indexes like numpy, core.py:280)
+        moves once per entry, with that entry's action.  Up to 4n entries -- every agent under all
+        four of those forms; int() accepts yet more spellings of a number ('00', ' 0'), and a dict
+        with more than 4n entries raises ValueError where the reference would run it."""
         n, R = self._num_agents, self._num_requests
         h_io, d_io, h_regen, d_regen = self._io_buffers()
-        io = h_io.numpy()                                    # row 0: actions, row 1: dict order
-        io[0] = 4
-        io[1] = -1
-        if len(action_dict) > self._engine.agent_slots:
-            raise ValueError(f"{len(action_dict)} dict entries for {self._engine.agent_slots} agent slots")
+        io = h_io.numpy()[0]                                 # [actions (n) | dict order (4n)]
+        io[:n] = 4
+        io[n:] = -1
+        if len(action_dict) > 4 * n:
+            raise ValueError(f"{len(action_dict)} action-dict entries: at most 4 per agent ({4 * n}) are supported")
         for s, (key, action) in enumerate(action_dict.items()):
             idx = agent_index(key, n)
             a = int(action)
             if not -9 <= a <= 8:                            # MOVES[action] (core.py:282)
                 raise IndexError("list index out of range")
-            io[1, s] = idx | ((a % 9 + 1) << 8)             # the entry's own action (a repeated agent)
-            io[0, idx] = a % 9                               # Python's negative-index wrap
+            io[n + s] = idx | ((a % 9 + 1) << 8)            # the entry's own action (a repeated agent)
+            io[idx] = a % 9                                  # Python's negative-index wrap
+        ol = max(n, len(action_dict))
         eng = self._engine
         if self._rendering:
             self._prev = self._snapshot()                    # core.py:270-272
@@ -199,7 +204,7 @@ class Warehouse(MultiAgentEnv):
         # back; then observations, rewards and dones come back in one copy.  Uploads are async
         # from pinned buffers on the launch stream (each is rewritten only after a later sync).
         d_io.copy_(h_io, non_blocking=True)
-        eng.step(d_io[0:1], order=d_io[1:2], phase=nat.WH_PHASE_PRE_REGEN)
+        eng.step(d_io[:, :n], order=d_io[:, n:n + ol], phase=nat.WH_PHASE_PRE_REGEN)
         n_in = int(eng.n_inactive[0].item())
         k = R - self._num_pickup_points + n_in
         rpos = np.random.choice(n_in, k, replace=False)                       # core.py:339-343

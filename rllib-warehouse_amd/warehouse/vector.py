@@ -108,7 +108,7 @@ class WarehouseVectorEnv:
 
     def vector_step(self, actions, mask=None, order=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, dict]:
         """actions [B,NA] int in 0..8 (values outside act as 4 = stay); `mask` [B] bool limits the
-        step to some envs; `order` [B,NA] int (-1 terminated) is each env's action-dict order --
+        step to some envs; `order` [B,OL] int (OL <= 4 NA, -1 padded) is each env's action-dict order --
         agents it leaves out are skipped as in the reference (core.py:279-300), None = every agent
         in ascending id order.  Returns env-owned (obs [B,NA,9R+1], rewards [B,NA], dones [B]
         bool, infos)."""
@@ -193,18 +193,19 @@ class WarehouseBaseEnv:
         and so does an agent id outside [-n, n) (agent_positions[idx], core.py:280); negative keys
         name agent n + key as numpy indexing does, and an agent named under two keys ('0' and 0)
         moves once per entry with that entry's action (each order entry carries its own action).
-        Limit (not the reference's): at most NA entries per env dict (one order entry per agent
-        slot); more raise ValueError, where the reference would accept up to 4n key forms."""
+        Up to 4n entries per env dict (every agent under the four key forms '0', 0, '-n', -n); a
+        longer dict (int() accepts more spellings, '00') raises ValueError where the reference runs it."""
         NA = self.vec.num_agents
+        width = max([NA] + [len(ad) for ad in action_dict.values()])
         acts = np.full((self.num_envs, NA), 4, np.int32)
-        order = np.full((self.num_envs, NA), -1, np.int32)
+        order = np.full((self.num_envs, width), -1, np.int32)
         mask = np.zeros(self.num_envs, bool)
         ascending = True            # every dict lists all agents of its env in ascending order
         for e, ad in action_dict.items():
             mask[e] = True
             n = int(self._n[e])
-            if len(ad) > NA:
-                raise ValueError(f"env {e}: {len(ad)} actions for {NA} agent slots")
+            if len(ad) > 4 * n:
+                raise ValueError(f"env {e}: {len(ad)} action-dict entries: at most 4 per agent ({4 * n}) are supported")
             for s, (a, v) in enumerate(ad.items()):
                 idx, v = agent_index(a, n), int(v)
                 if not -9 <= v < 9:

@@ -131,9 +131,10 @@ int main() {
   }
 
   // ---- argument checks of the other entry points (empty batches run nothing)
-  EXPECT(wh_step(&medium, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 7, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_step(&medium, 4, dummy_state, nullptr, nullptr, rew, dn, nullptr, nullptr, WH_PHASE_ALL, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_step(&medium, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, WH_PHASE_ALL, 0, 0, nullptr) == WH_OK);
+  EXPECT(wh_step(&medium, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 7, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_step(&medium, 4, dummy_state, nullptr, nullptr, 0, rew, dn, nullptr, nullptr, WH_PHASE_ALL, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_step(&medium, 4, dummy_state, (const int32_t*)dummy_state, (const int32_t*)dummy_state, 37, rew, dn, nullptr, nullptr, WH_PHASE_ALL, 0, 0, nullptr) == WH_EINVAL);   // order rows > 4 NA
+  EXPECT(wh_step(&medium, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, WH_PHASE_ALL, 0, 0, nullptr) == WH_OK);
   EXPECT(wh_policy(&medium, 0, nullptr, 9, 0.0f, nullptr, 0, 0, nullptr) == WH_EINVAL);
   EXPECT(wh_policy(&medium, 0, nullptr, WH_POLICY_GREEDY, -0.1f, nullptr, 0, 0, nullptr) == WH_EINVAL);
   EXPECT(wh_policy(&medium, 0, nullptr, WH_POLICY_GREEDY, 0.0f, nullptr, 0, 0, nullptr) == WH_OK);
@@ -146,14 +147,14 @@ int main() {
   EXPECT(wh_unpack(&medium, 4, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) == WH_EINVAL);
   EXPECT(wh_observe(&medium, 0, nullptr, nullptr, nullptr) == WH_OK);
   EXPECT(wh_observe(&bad, 0, nullptr, nullptr, nullptr) == WH_EINVAL);
-  EXPECT(wh_vector_step(&medium, 4, dummy_state, nullptr, nullptr, nullptr, rew, dn, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_vector_step(&medium, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_OK);
+  EXPECT(wh_vector_step(&medium, 4, dummy_state, nullptr, nullptr, 0, nullptr, rew, dn, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_vector_step(&medium, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_OK);
   const int32_t acts[32] = {0};
   alignas(16) unsigned char xbuf[64];
-  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, nullptr, nullptr, nullptr, rew, dn, rew, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, acts, nullptr, nullptr, rew, dn, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, acts, nullptr, nullptr, rew, dn, xbuf + 4, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
-  EXPECT(wh_vector_step_x(&medium, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_OK);
+  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, nullptr, nullptr, 0, nullptr, rew, dn, rew, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, acts, nullptr, 0, nullptr, rew, dn, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_vector_step_x(&medium, 4, dummy_state, acts, nullptr, 0, nullptr, rew, dn, xbuf + 4, nullptr, 1, 0, 0, 0, nullptr) == WH_EINVAL);
+  EXPECT(wh_vector_step_x(&medium, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 0, 0, 0, nullptr) == WH_OK);
   EXPECT(wh_sampler_step(&medium, 0, nullptr, 5, 0.0f, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr) == WH_EINVAL);
   EXPECT(wh_sampler_rollout(&medium, 4, dummy_state, 3, WH_POLICY_GREEDY, 0.0f, rew, dn, nullptr, nullptr, 0, 0, 0, nullptr) == WH_EINVAL);
   EXPECT(wh_sampler_rollout(&medium, 0, nullptr, 3, WH_POLICY_GREEDY, 0.0f, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr) == WH_OK);

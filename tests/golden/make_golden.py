@@ -14,7 +14,8 @@ It never runs on the GPU box and nothing imports it at test time; the tests read
   and dones.  `ord_*` files do the same with shuffled/partial action dicts (`core.py:279`);
   `keys_*` with the key forms `int(key)` accepts beyond "0".."n-1" (`core.py:280`): int keys,
   negative keys (numpy wraps them to n + key) and one agent named under two keys in one dict
-  (moved once per entry, each with its own action).
+  (moved once per entry, each with its own action); `long_*` with dicts of up to 4n entries
+  (agents under several of the four forms at once: several moves of one agent in one step).
 * G2 `g2_<variant>.npz` -- single transitions from adversarial hand-built states (agents packed
   on a few cells, on pickup cells, carrying next to their delivery cell, timers about to expire,
   t about to reach T) with random actions and dict orders.
@@ -196,14 +197,17 @@ def run_g1(variant, n, seed, steps=200, shuffle=False):
     return arr
 
 
-def run_keys(variant, n, seed, steps=200):
+def run_keys(variant, n, seed, steps=200, long=False):
     """A G1 episode whose action dicts mix key forms: str(a), int a, str(a - n), int(a - n), so some
     dicts name an agent under two keys (both entries act).  Per step the dict's entries are recorded
     as key_form (0 str, 1 int, 2 negative str, 3 negative int; -1 = no entry), key_agent (the agent
-    the key names) and key_act (the entry's action, -9..8)."""
+    the key names) and key_act (the entry's action, -9..8).  long=True (`long_*` fixtures): dicts of
+    up to 4n entries -- agents named under several, up to all four, key forms, so one agent moves
+    several times in one step -- and every 10th dict holds all 4n keys."""
     cls = VARIANTS[variant]
     np.random.seed(seed)
-    act_rng = np.random.RandomState(20_000 + 31 * seed + n)
+    act_rng = np.random.RandomState(20_000 + 31 * seed + n + (7_777 if long else 0))
+    width = 4 * n if long else n
     env = cls(n)
     R = env._num_requests
     with DrawRecorder() as rec:
@@ -216,12 +220,14 @@ def run_keys(variant, n, seed, steps=200):
     s0 = canon_state(env)
     dup_steps = 0
     for s in range(steps):
-        m = int(act_rng.randint(1, n + 1))
-        form = np.full(n, -1, np.int32)
-        agent = np.full(n, -1, np.int32)
-        act = np.zeros(n, np.int32)
+        m = int(act_rng.randint(1, width + 1)) if not (long and s % 10 == 9) else 64 * width
+        form = np.full(width, -1, np.int32)
+        agent = np.full(width, -1, np.int32)
+        act = np.zeros(width, np.int32)
         action_dict = {}
         for j in range(m):
+            if len(action_dict) == width:
+                break
             a, f, v = int(act_rng.randint(0, n)), int(act_rng.randint(0, 4)), int(act_rng.randint(-9, 9))
             key = [str(a), a, str(a - n), a - n][f]
             if key in action_dict:
@@ -400,6 +406,13 @@ def main_keys():
     print("wrote keys_* fixtures to", HERE)
 
 
+def main_long():
+    for variant, n in (("small", 4), ("medium", 8), ("large", 16)):
+        arr = run_keys(variant, n, 9, long=True)
+        np.savez_compressed(os.path.join(HERE, f"long_{variant}_n{n}_s9.npz"), **arr)
+    print("wrote long_* fixtures to", HERE)
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     for variant, nmax in (("small", 4), ("medium", 9), ("large", 16)):
@@ -418,6 +431,9 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["keys"]:   # (added in round 4: only the keys_* fixtures)
         main_keys()
+    elif sys.argv[1:] == ["long"]:   # (added in round 6: only the long_* fixtures)
+        main_long()
     else:
         main()
         main_keys()
+        main_long()

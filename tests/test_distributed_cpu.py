@@ -1,6 +1,7 @@
 """The multi-GPU path on CPU with gloo, world size 2, through bench.py's own plumbing: rank_info()
 from the torch.distributed.run environment, shard_offset() (rank r owns global env ids
-[r*B, (r+1)*B)), timed_window() (barrier + sync on both sides, max over ranks) and aggregate_rate();
+[r*B, (r+1)*B)), timed_window() (barrier + sync on both sides, a common start, the union of the
+ranks' windows) and aggregate_rate();
 the shard-invariance contract (philox draws keyed by global env id) is checked with the oracle
 standing in for each rank's GPU."""
 import os
@@ -102,6 +103,57 @@ def test_two_rank_shards_equal_single_batch(tmp_path):
             ob.reset(L, S, d, mask=done)
     np.testing.assert_array_equal(sharded, S.pos)
     assert total == ref_total
+
+
+def _skew_worker(rank, world, port, out):
+    """Rank 1 opens its window 0.3 s after the common start and works 0.1 s; rank 0 works 0.2 s from
+    the start: the ranks' windows do not overlap at all, the slowest rank's own window is 0.2 s, and
+    the union -- what the two shards were processed in -- is ~0.4 s."""
+    import json
+    import time
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    work = 0.2 if rank == 0 else 0.1
+    w = bench.timed_window(lambda: time.sleep(work), lambda: None, world, dist,
+                           start_delay=0.0 if rank == 0 else 0.3)
+    if rank == 0:
+        json.dump({"union": float(w), "rate": bench.aggregate_rate(world, 1000, 8, 10, w),
+                   "desc": w.describe(1000 * 8 * 10)}, open(out, "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_union_window_sets_the_aggregate(tmp_path):
+    """bench.timed_window with deliberately skewed ranks: `value` comes from the union of the ranks'
+    windows on the shared monotonic clock, not from the slowest rank's own window (which would
+    count two serialised windows as concurrent); overlap_frac reports that they never overlapped."""
+    import json
+
+    out = str(tmp_path / "w.json")
+    mp.start_processes(_skew_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    r = json.load(open(out))
+    d = r["desc"]
+    assert max(d["per_rank_s"]) == pytest.approx(0.2, abs=0.05)
+    assert r["union"] >= 0.39 and r["union"] == pytest.approx(d["union_s"])
+    assert r["union"] > max(d["per_rank_s"]) + 0.15
+    assert r["rate"] == pytest.approx(2 * 1000 * 8 * 10 / r["union"])
+    assert d["overlap_frac"] == 0.0
+    assert d["rank_start_offsets_us"][0] == 0.0 and d["rank_start_offsets_us"][1] >= 0.29e6
+    assert len(d["per_rank_rate"]) == 2
+
+
+def test_union_window_of_concurrent_ranks():
+    """Two ranks whose windows coincide: union == the slowest rank, overlap 1."""
+    import bench
+
+    w = bench.WindowTime([10.0, 10.0], [10.5, 10.4])
+    assert float(w) == pytest.approx(0.5) and w.overlap == pytest.approx(0.8)
+    w = bench.WindowTime([1.0], [1.25])
+    assert float(w) == pytest.approx(0.25) and w.overlap == 1.0
 
 
 def _bench_env(**extra):

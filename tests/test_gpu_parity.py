@@ -364,12 +364,13 @@ def test_dropin_key_forms_match_reference(wh, variant, n):
         env.step({str(-n - 1): 0})
     with pytest.raises(IndexError):
         env.step({str(n): 0})
-    # the documented limit (Warehouse.step): at most agent_slots entries per dict -- the reference would
-    # accept up to 4n key forms, this build refuses more than one order entry per slot
-    over = {str(i): 4 for i in range(n)}
-    over[0] = 4
+    # up to 4n entries (every agent under its four key forms) run; a fifth spelling of a number
+    # ('00': int() accepts it) is past the documented limit and raises ValueError
+    full = {k: 4 for i in range(n) for k in (str(i), i, str(i - n), i - n)}
+    env.step(full)
+    full["00"] = 4
     with pytest.raises(ValueError):
-        env.step(over)
+        env.step(full)
 
 
 def test_dropin_train_variant_matches_oracle(wh):

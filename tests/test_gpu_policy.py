@@ -220,7 +220,9 @@ def frag_reference(rows_f32, kq):
 
 
 @pytest.mark.parametrize("variant,na,B", [("small", 4, 100), ("medium", 8, 61), ("large", 16, 37),
-                                          ("medium", 9, 150), ("large", 5, 70), ("small", 3, 131)])
+                                          ("medium", 9, 150), ("large", 5, 70), ("small", 3, 131),
+                                          ("small", 1, 130), ("medium", 1, 70), ("large", 1, 200),
+                                          ("medium", 2, 99), ("large", 2, 77)])
 def test_observe_x_fragments_and_forward_x(wh, variant, na, B):
     """wh_observe_x writes exactly the bf16 fragment image of wh_observe's rows (bias columns 1.0,
     padding 0, ragged last tile), and wh_mlp_forward_x on it gives bit-identical logits and actions

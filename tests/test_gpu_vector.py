@@ -671,7 +671,8 @@ def test_sampler_observation_rows_equal_wh_observe(wh, variant, na, train, B):
 
 @pytest.mark.parametrize("variant,na,train,B", [("medium", 8, False, 4096), ("medium", 9, True, 1000),
                                                 ("large", 16, False, 777), ("small", 4, True, 2049),
-                                                ("small", 3, False, 129)])
+                                                ("small", 3, False, 129), ("small", 1, False, 150),
+                                                ("medium", 2, False, 333)])
 def test_vector_step_x_equals_vector_step_then_observe_x(wh, variant, na, train, B):
     """wh_vector_step_x (the step launch writing the policy's fragment-order operand) == the same
     wh_vector_step without rows followed by wh_observe_x, byte for byte, with equal rewards, dones

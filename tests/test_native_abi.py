@@ -121,16 +121,27 @@ def test_query_rejects_bad_configs():
         _native.query(_native.make_config(14, 4, (4, 8), 2, 200, 200))
 
 
-def test_no_cpu_fallback():
+def test_no_silent_fallback_between_engines():
+    """Without a HIP device the classes run on the host engine (libwarehouse_host.so, product C++),
+    never on the oracle; naming a HIP device on such a host raises instead of moving to the host,
+    and the device-only policy network refuses the host.  With a HIP device the default is the
+    gfx950 library."""
     import torch
     import warehouse
+    import warehouse.policy  # noqa: F401
+    from warehouse import _native
 
     if torch.cuda.is_available():
-        pytest.skip("a GPU is visible")
+        env = warehouse.BatchedWarehouse("small", 4, 2)
+        assert not env.host and env._lib is _native.lib()
+        return
+    env = warehouse.BatchedWarehouse("small", 4, 2)
+    assert env.host and env._lib is _native.host_lib() and env.device.type == "cpu"
+    assert warehouse.WarehouseSmall(2)._engine.host
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        warehouse.BatchedWarehouse("small", 4, 2, device="cuda")
     with pytest.raises(RuntimeError, match="no CPU fallback"):
-        warehouse.BatchedWarehouse("small", 4, 2)
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        warehouse.WarehouseSmall(2)
+        warehouse.policy.MLPPolicy("small")
 
 
 def test_mlp_query_shapes():
