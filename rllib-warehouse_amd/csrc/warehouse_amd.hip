@@ -1269,9 +1269,16 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
             atomicOr(occ_at(c), bop3<TA & TB>(mok, 1u << (c & 31u), 0u));
             const uint32_t dxy = c ^ p;
             if constexpr (UKEY) {
-              uint32_t z;   // 1 for a stay: v_ffbl of 0 is ~0
-              asm("v_ffbl_b32 %0, %1" : "=v"(z) : "v"(dd));
-              sk[sidx] = bop3<~TA | (TB ^ TC)>(mok, kpr, z >> 31);
+              if constexpr (REV) {
+                uint32_t z;   // 1 for a stay: v_ffbl of 0 is ~0
+                asm("v_ffbl_b32 %0, %1" : "=v"(z) : "v"(dd));
+                sk[sidx] = bop3<~TA | (TB ^ TC)>(mok, kpr, z >> 31);
+              } else {
+                // No lane of the wave has co-located agents: a later agent can then never make the
+                // same move p -> c as an accepted one (it would have to stand on p too), so every
+                // stored key may carry the flipped low bit a stay's needs -- one op instead of three
+                sk[sidx] = bop3<~TA | (TB ^ TC)>(mok, kpr, 1u);
+              }
             } else {
               if constexpr (REV) rk[sidx] = bop3<~TA | TB>(mok, (c & XY16) | ((p & XY16) << 8), 0u);
               xk[sidx] = bop3<~TA | (TB ^ TC)>(mok, ukey, 0xFE000000u);
@@ -1291,10 +1298,13 @@ __device__ __forceinline__ bool step_env(Regs<C>& s, Lds<C>& L, const uint32_t (
           // pin the hoisted block to this basic block (LLVM would sink it back to its only use)
           if constexpr (HOIST) asm volatile("" : "+v"(rblk0.x), "+v"(rblk0.y), "+v"(rblk0.z), "+v"(rblk0.w));
         };
+        // REV: the exact loop for waves with co-located agents (reverse keys in the two-key form; in
+        // the one-key form every stay's key flipped), else the loop for waves without any (no reverse
+        // keys / every key flipped).  From kRevSplitMaxNam agents on a single (exact) loop.
 #ifdef WH_FORCE_NOREV   // timing-only A/B builds: never the reverse-key loop (wrong with co-located agents)
-        if (!LAZY && !UKEY)
+        if (!LAZY)
 #else
-        if (!UKEY && (!LAZY || C::NAM > kRevSplitMaxNam || WH_RARE(__any(lg->cm != 0u))))
+        if (!LAZY || C::NAM > kRevSplitMaxNam || WH_RARE(__any(lg->cm != 0u)))
 #endif
         {
 #ifdef WH_COUNT_REV   // A/B builds: count the wave-steps that take the reverse-key loop (wh_check_read)
@@ -2834,7 +2844,10 @@ bool fused_ok(void (*kern)(StepParams, float*)) {
 // workgroups, 178 vs 137.5 us per sampler step for the two launches; Small-4 13.2 vs 15.1, Medium-8
 // 34.7 vs 40.3 (profiles/r05_step3_ab.txt).  So configurations with more than 4 KB of rows per env
 // take the two launches.
-bool fuse_rows(const Geometry& g) { return 4 * g.NA * (9 * g.R + 1) <= 4096; }
+#ifndef WH_FUSE_ROWS_MAX   // (A/B builds: -DWH_FUSE_ROWS_MAX=<bytes of rows per env> moves the limit)
+#define WH_FUSE_ROWS_MAX 4096
+#endif
+bool fuse_rows(const Geometry& g) { return 4 * g.NA * (9 * g.R + 1) <= WH_FUSE_ROWS_MAX; }
 
 const Kernels* pick(const Geometry& g) {
   const Kernels* best = nullptr;
