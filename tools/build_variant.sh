@@ -5,4 +5,4 @@
 cd "$(dirname "$0")/../rllib-warehouse_amd/csrc" || exit 2
 NAME=$1; shift
 mkdir -p ../../build_ab
-make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*"
+make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*" lib
