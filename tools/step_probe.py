@@ -17,6 +17,28 @@ import torch  # noqa: E402
 import warehouse  # noqa: E402
 
 
+def positioning(T, steps, launches, cross):
+    """Untimed positioning steps before each timed launch (0 = none): with cross, t + K/2 = T (mod T),
+    so the launch's middle step ends the episode."""
+    t, out = 0, []
+    for _ in range(launches):
+        pos = (T - steps // 2 - t) % T if cross else 0
+        out.append(pos)
+        t = (t + pos + steps) % T
+    return out
+
+
+def timed_dispatches(T, steps, launches, cross):
+    """Indices, among this probe's k_step dispatches in issue order, of the timed launches (each
+    positioning rollout is one k_step dispatch of its own)."""
+    idx, i = [], 0
+    for pos in positioning(T, steps, launches, cross):
+        i += pos > 0
+        idx.append(i)
+        i += 1
+    return idx
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variant", default="medium")
@@ -45,13 +67,9 @@ def main():
     s = torch.cuda.current_stream(dev)
     times = []
     T = int(env.geometry["T"])
-    t = 0
-    for _ in range(a.launches):
-        if a.cross:   # t + K/2 = T (mod T): the launch's middle step ends the episode
-            pos = (T - a.steps // 2 - t) % T
-            if pos:
-                env.rollout(pos, a.policy, 0.0)
-            t = (t + pos + a.steps) % T
+    for pos in positioning(T, a.steps, a.launches, a.cross):
+        if pos:
+            env.rollout(pos, a.policy, 0.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         launch()
