@@ -343,8 +343,11 @@ __device__ __forceinline__ uint32_t action_of(uint32_t d) {
 #define WH_RARE(x) (x)
 #endif
 
-// Phase labels in the device assembly for instruction-count analysis; -DWH_NO_PHASE_MARKS drops them.
-#ifndef WH_NO_PHASE_MARKS
+// Phase labels in the device assembly for instruction-count analysis (`make asm` defines
+// WH_PHASE_MARKS).  Not in the library: each label is an asm volatile with a memory clobber, a
+// scheduling barrier for memory operations -- without them Large-16 runs 0.9 % and Medium-8 0.3 %
+// faster per 200-step launch (profiles/r06_nomarks_ab.txt).
+#ifdef WH_PHASE_MARKS
 #define WH_PHASE_MARK(name) asm volatile("; PHASE " #name ::: "memory")
 #else
 #define WH_PHASE_MARK(name) ((void)0)
