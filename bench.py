@@ -550,10 +550,10 @@ def measure_sampler(env, K, W, dev, world, dist):
 def sampler_fused(env):
     """Whether wh_sampler_step runs as one k_sampler launch for env's shape (warehouse_amd.hip
     wh_sampler_step: the fast step instance -- every slot live, even agent count -- and at most 4 KB of
-    rows per env, fuse_rows), else the step launch + k_observe."""
+    rows per env, fuse_rows; Large builds no k_sampler, kSamplerBuilt), else the step launch + k_observe."""
     NA = env.agent_slots
     return (NA % 2 == 0 and env.layout.kernel_agents == NA and not env.train
-            and 4 * NA * env.obs_len <= 4096)
+            and 4 * NA * env.obs_len <= 4096 and int(env.geometry["R"]) < 16)
 
 
 def sampler_line(env, Ks, el, split, world, variant, words, fused):
@@ -823,7 +823,8 @@ def vector_leg(env, K, W, dev, world, dist, label, order=None):
     B, NA = env.B, env.agent_slots
     el, vms = measure_vector(env, K, W, dev, world, dist, order=order)
     words = env.layout.words_per_env
-    fused = sampler_fused(env) or (order is not None and 4 * NA * env.obs_len <= 4096 and NA % 2 == 0)
+    fused = sampler_fused(env) or (order is not None and 4 * NA * env.obs_len <= 4096 and NA % 2 == 0
+                                   and int(env.geometry["R"]) < 16)
     vec_b = (B * NA * env.obs_len * 4 + (2 if fused else 3) * B * 4 * words + B * (4 * NA + 1) + B * NA * 4
              + (0 if order is None else 4 * order.numel()))
     return {"workload": label, "value": aggregate_rate(world, B, NA, K, el), "unit": "agent-steps/s", "steps": K,
@@ -835,7 +836,7 @@ def vector_leg(env, K, W, dev, world, dist, label, order=None):
                                  "launches) + rewards + dones + actions (+ order rows)"}}
 
 
-def step_roofline(m, variant, NA, policy, mode, envs=65536):
+def step_roofline(m, variant, NA, policy, mode, envs):
     """The bench line's `roofline` for the timed launches of measure() (dict m).  achieved / peak /
     frac are the contract's HBM figures (algorithmic bytes per launch / the launch's event-timed
     duration, against 8 TB/s); `valu` is the chip-level VALU issue roofline of the same launch (from
@@ -1175,7 +1176,7 @@ def main():
                         "launch": "self-launched ranks" if os.environ.get("WH_BENCH_SELF_LAUNCHED") else
                                   ("torch.distributed.run" if world > 1 else "single process")},
             "window": m["window"],
-            "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode),
+            "roofline": step_roofline(m, args.variant, NA, args.policy, args.mode, args.envs),
             "alt_launch_mode": alt,
             "desync_episodes": desync,
             "sampler_path": sampler,

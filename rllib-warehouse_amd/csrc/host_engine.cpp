@@ -8,7 +8,8 @@
 // (packed state layout, injected draws, the philox draw contract of the device kernels) -- not a
 // translation of the test oracle, which it never calls.  Every pointer is host memory and `stream`
 // is ignored.  Entry points the CPU has no use for (the policy network, the fragment operand, the
-// fused sampler launches, prepared launches, assert mode) return WH_ENOTSUP.
+// two-stream sampler step wh_sampler_step_to, prepared launches, assert mode) return WH_ENOTSUP;
+// wh_sampler_step / wh_sampler_rollout run as policy + vector step per env.
 //
 // The state is the device's packed word planes (state[w * B + e]), so a state can move between the
 // two engines with a plain copy, and the philox draws follow the device's stream layout word for

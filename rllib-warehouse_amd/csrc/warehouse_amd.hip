@@ -74,6 +74,9 @@ constexpr bool kBiasAddr = false;
 #define WH_OBS_EB0 4
 #endif
 constexpr int kObsEB[4] = {WH_OBS_EB0, 8, 16, 64};   // the observation kernel's instances
+#ifndef WH_FUSE_ROWS_MAX   // rows per env (bytes) up to which the sampler routes fuse step + rows (fuse_rows)
+#define WH_FUSE_ROWS_MAX 4096
+#endif
 // Observation stores (same-box A/Bs, tools/obs_bench.py, sampler_probe.py and policy_probe.py;
 // profiles/r05_l16rows_ab.txt, r05_ntm8_ab.txt, r05_ntsel_ab.txt): f32 rows nontemporal for rows of
 // <= 1 KB or > 4 KB per env (Small / Large: observe -5 % / -2 %, Large-16's sampler route -3 %,
@@ -2761,6 +2764,13 @@ struct Kernels {
   int tblw, nv;
 };
 
+// Large (R = 16) dispatches no k_sampler: with 16 agent slots its rows (9.3 KB per env) pass the fuse
+// limit, and with 2-8 slots the step code spills at two waves per SIMD (220-544 B of scratch,
+// tools/kernel_resources.py), which fused_ok() refuses.  Those instances are not built (unless an A/B
+// build raises the limit), so no kernel with a private segment is left in the dict-order route.
+template <class C>
+constexpr bool kSamplerBuilt = C::R < 16 || WH_FUSE_ROWS_MAX > 4096;
+
 template <int D, int R, int NR, int NAM>
 Kernels make_kernels() {
   using C = Cfg<D, R, NR, NAM>;
@@ -2778,10 +2788,12 @@ Kernels make_kernels() {
     k.step_fast[0] = k_step<C, POL_EXTERNAL, false, true>;
     k.step_fast[1] = k_step<C, POL_GREEDY, false, true>;
     k.step_fast[2] = k_step<C, POL_RANDOM, false, true>;
-    k.sampler[0] = k_sampler<C, POL_EXTERNAL, false, true>;
-    k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
-    k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
-    if constexpr (sampler_fits) {
+    if constexpr (kSamplerBuilt<C>) {
+      k.sampler[0] = k_sampler<C, POL_EXTERNAL, false, true>;
+      k.sampler[1] = k_sampler<C, POL_GREEDY, false, true>;
+      k.sampler[2] = k_sampler<C, POL_RANDOM, false, true>;
+    }
+    if constexpr (sampler_fits && kSamplerBuilt<C>) {
       k.sampler_multi[1] = k_sampler<C, POL_GREEDY, false, true, true>;
       k.sampler_multi[2] = k_sampler<C, POL_RANDOM, false, true, true>;
     }
@@ -2789,12 +2801,13 @@ Kernels make_kernels() {
     k.step_fast[1] = k.step_fast[2] = nullptr;
   }
   k.step_ordered = k_step<C, POL_EXTERNAL, true, false>;
-  k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
-  // the dict-order instance also holds the entries' move keys (OKeys: 4 * NAM x 512 bytes)
-  if constexpr (sizeof(Lds<C>) + sizeof(SampLds<C, 1>) + sizeof(OKeys<C>) <= 160 * 1024)
-    k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
-  else
-    k.vsampler[1] = nullptr;
+  k.vsampler[0] = k.vsampler[1] = nullptr;
+  if constexpr (kSamplerBuilt<C>) {
+    k.vsampler[0] = k_sampler<C, POL_EXTERNAL, false, false>;
+    // the dict-order instance also holds the entries' move keys (OKeys: 4 * NAM x 512 bytes)
+    if constexpr (sizeof(Lds<C>) + sizeof(SampLds<C, 1>) + sizeof(OKeys<C>) <= 160 * 1024)
+      k.vsampler[1] = k_sampler<C, POL_EXTERNAL, true, false>;
+  }
   k.reset = k_reset<C>;
   k.observe[0] = k_observe<C, kObsEB[0]>;
   k.observe[1] = k_observe<C, kObsEB[1]>;
@@ -2844,12 +2857,10 @@ bool fused_ok(void (*kern)(StepParams, float*)) {
 
 // The fused step + rows launch pays while an env's rows are small: at Large-16 (9.3 KB of rows per
 // env, one 512-lane workgroup per CU by LDS) it streams the rows slower than k_observe's small
-// workgroups, 178 vs 137.5 us per sampler step for the two launches; Small-4 13.2 vs 15.1, Medium-8
-// 34.7 vs 40.3 (profiles/r05_step3_ab.txt).  So configurations with more than 4 KB of rows per env
-// take the two launches.
-#ifndef WH_FUSE_ROWS_MAX   // (A/B builds: -DWH_FUSE_ROWS_MAX=<bytes of rows per env> moves the limit)
-#define WH_FUSE_ROWS_MAX 4096
-#endif
+// workgroups -- 165 vs 127 us per sampler step for the two launches (profiles/r06_l16fuse_ab.txt,
+// with the fused instance free of scratch); Small-4 13.2 vs 15.1, Medium-8 34.7 vs 40.3
+// (profiles/r05_step3_ab.txt).  So configurations with more than WH_FUSE_ROWS_MAX bytes of rows per
+// env take the two launches.
 bool fuse_rows(const Geometry& g) { return 4 * g.NA * (9 * g.R + 1) <= WH_FUSE_ROWS_MAX; }
 
 const Kernels* pick(const Geometry& g) {

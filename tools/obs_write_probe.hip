@@ -5,14 +5,25 @@
 // one workgroup per CU).  MODE 0: gather from LDS (k_observe's loop); MODE 1: the same with the LDS
 // reads of U iterations issued before their stores; MODE 2: stores of a constant (no gathers).
 //   hipcc --offload-arch=gfx950 -O3 tools/obs_write_probe.hip -o tools/obs_write_probe_bin
+//   hipcc --offload-arch=gfx950 -O3 -DPROBE_LARGE tools/obs_write_probe.hip -o tools/obs_write_probe_large   (Large-16 rows)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
 
+#ifdef PROBE_LARGE   // Large-16 rows: 16 x 145 floats per env (round 6: what bounds k_observe<Large>?)
+constexpr int NA = 16, L = 145, IMG = 148, PER_ENV = NA * L, QE = PER_ENV / 4;   // 580 float4 per env
+#else
 constexpr int NA = 8, L = 82, IMG = 84, PER_ENV = NA * L, QE = PER_ENV / 4;   // 164 float4 per env
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int THREADS, int ENVS, int MODE, int U>
+template <bool NT>
+__device__ __forceinline__ void st(f32x4* p, f32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int THREADS, int ENVS, int MODE, int U, bool NT>
 __global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int64_t B) {
   __shared__ uint8_t img[ENVS][IMG];
   __shared__ uint32_t lim[ENVS];
@@ -32,7 +43,7 @@ __global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int6
   const uint32_t magic = 0xFFFFFFFFu / QE + 1u;
   f32x4* out4 = reinterpret_cast<f32x4*>(obs + e0 * PER_ENV);
   if (MODE == 2) {
-    for (uint32_t q = tid; q < total; q += THREADS) out4[q] = (f32x4){1.0f, 2.0f, 3.0f, 4.0f};
+    for (uint32_t q = tid; q < total; q += THREADS) st<NT>(&out4[q], (f32x4){1.0f, 2.0f, 3.0f, 4.0f});
     return;
   }
   auto value = [&](uint32_t q) -> f32x4 {
@@ -50,7 +61,7 @@ __global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int6
     return v;
   };
   if (MODE == 0) {
-    for (uint32_t q = tid; q < total; q += THREADS) out4[q] = value(q);
+    for (uint32_t q = tid; q < total; q += THREADS) st<NT>(&out4[q], value(q));
   } else {
     uint32_t q = tid;
     for (; q + (U - 1) * THREADS < total; q += U * THREADS) {
@@ -58,23 +69,23 @@ __global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int6
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = value(q + u * THREADS);
 #pragma unroll
-      for (int u = 0; u < U; ++u) out4[q + u * THREADS] = v[u];
+      for (int u = 0; u < U; ++u) st<NT>(&out4[q + u * THREADS], v[u]);
     }
-    for (; q < total; q += THREADS) out4[q] = value(q);
+    for (; q < total; q += THREADS) st<NT>(&out4[q], value(q));
   }
 }
 
-template <int THREADS, int ENVS, int MODE, int U = 1>
+template <int THREADS, int ENVS, int MODE, int U = 1, bool NT = false>
 void run(float* obs, int64_t B, const char* name) {
   const unsigned grid = (unsigned)((B + ENVS - 1) / ENVS);
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
     hipEventRecord(a, 0);
-    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_probe<THREADS, ENVS, MODE, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms;
@@ -90,6 +101,19 @@ int main() {
   const int64_t B = 65536;
   float* obs;
   hipMalloc(&obs, (size_t)B * PER_ENV * 4);
+#ifdef PROBE_LARGE
+  run<256, 4, 0, 1, true>(obs, B, "Large k_observe shape (4 envs), gather, nt");
+  run<256, 4, 1, 2, true>(obs, B, "Large 4 envs, gather unroll 2, nt");
+  run<256, 4, 2, 1, true>(obs, B, "Large 4 envs, constant stores, nt");
+  run<256, 4, 0, 1, false>(obs, B, "Large 4 envs, gather, plain");
+  run<256, 4, 2, 1, false>(obs, B, "Large 4 envs, constant stores, plain");
+  run<256, 8, 0, 1, true>(obs, B, "Large 8 envs, gather, nt");
+  run<256, 8, 2, 1, true>(obs, B, "Large 8 envs, constant stores, nt");
+  run<512, 8, 1, 2, true>(obs, B, "Large 512 lanes 8 envs, gather unroll 2, nt");
+  run<512, 8, 2, 1, true>(obs, B, "Large 512 lanes 8 envs, constant stores, nt");
+  run<1024, 16, 2, 1, true>(obs, B, "Large 1024 lanes 16 envs, constant stores, nt");
+  return 0;
+#endif
   run<256, 16, 0>(obs, B, "k_observe shape, gather");
   run<256, 16, 2>(obs, B, "k_observe shape, constant stores");
   run<256, 64, 0>(obs, B, "256 lanes 64 envs, gather");
