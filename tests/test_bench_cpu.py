@@ -44,12 +44,12 @@ def test_step_roofline_names_the_binding_resource(monkeypatch):
     monkeypatch.setattr(bench, "load_profile", lambda tag: prof)
     m = dict(achieved_gbs=1000.0, kernel_ms=0.05, launches=1, steps_per_launch=20, bytes_per_launch=5.8e7,
              bytes_per_env_step=44.0, host_fixed_us=14.0)
-    r = bench.step_roofline(m, "medium", 8, "greedy", "fused")
+    r = bench.step_roofline(m, "medium", 8, "greedy", "fused", 65536)
     want = 1.8e7 / 50e-6 / 1e9 / (1024 * 1.2)
     assert r["valu"]["frac"] == r["valu_frac"] and abs(r["valu_frac"] - want) < 1e-12
     assert r["frac"] == r["hbm_frac"] == 1000.0 / 8000.0 and r["unit"] == "GB/s"
     assert r["bound"] == "valu" and r["valu_frac"] > r["hbm_frac"]
     assert abs(r["issue"]["single_wave_issue_occupancy"] - 1.8e7 / 2.8e7) < 1e-12
     monkeypatch.setattr(bench, "load_profile", lambda tag: None)
-    r = bench.step_roofline(m, "medium", 8, "greedy", "fused")
+    r = bench.step_roofline(m, "medium", 8, "greedy", "fused", 65536)
     assert r["bound"] == "hbm" and r["valu"] is None
