@@ -75,6 +75,78 @@ __global__ __launch_bounds__(THREADS) void k_probe(float* __restrict__ obs, int6
   }
 }
 
+// Persistent form (round 6, Large rows): GRID workgroups; CONTIG: workgroup w writes the groups of
+// envs [w * B / GRID, (w + 1) * B / GRID) in order (one long sequential stream per workgroup), else
+// groups w, w + GRID, ... (interleaved).  Constant stores: the write shape alone.
+template <int THREADS, int ENVS, bool CONTIG, bool NT>
+__global__ __launch_bounds__(THREADS) void k_probe_p(float* __restrict__ obs, int64_t B) {
+  const int tid = threadIdx.x;
+  const int64_t ng = (B + ENVS - 1) / ENVS;
+  const int64_t per = (ng + gridDim.x - 1) / gridDim.x;
+  const int64_t g0 = CONTIG ? blockIdx.x * per : blockIdx.x;
+  const int64_t g1 = CONTIG ? (g0 + per < ng ? g0 + per : ng) : ng;
+  const int64_t gs = CONTIG ? 1 : gridDim.x;
+  for (int64_t g = g0; g < g1; g += gs) {
+    f32x4* out4 = reinterpret_cast<f32x4*>(obs + g * ENVS * PER_ENV);
+    for (uint32_t q = tid; q < (uint32_t)(ENVS * QE); q += THREADS) st<NT>(&out4[q], (f32x4){1.0f, 2.0f, 3.0f, 4.0f});
+  }
+}
+
+// Grid-stride sweep over the whole buffer (the fill_ / memset pattern): U stores per iteration.
+template <int THREADS, int U, bool NT>
+__global__ __launch_bounds__(THREADS) void k_sweep(float* __restrict__ obs, int64_t n4) {
+  f32x4* out4 = reinterpret_cast<f32x4*>(obs);
+  const int64_t stride = (int64_t)gridDim.x * THREADS;
+  for (int64_t q = (int64_t)blockIdx.x * THREADS + threadIdx.x; q < n4; q += U * stride) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q + u * stride < n4) st<NT>(&out4[q + u * stride], (f32x4){1.0f, 2.0f, 3.0f, 4.0f});
+  }
+}
+
+template <int THREADS, int U, bool NT>
+void run_s(float* obs, int64_t B, unsigned grid, const char* name) {
+  const int64_t n4 = B * (int64_t)QE;
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_sweep<THREADS, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, n4);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(a, 0);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_sweep<THREADS, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, n4);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    best = ms / 20 < best ? ms / 20 : best;
+  }
+  const double bytes = (double)B * PER_ENV * 4;
+  printf("%-44s threads=%4d unroll=%d grid=%6u: %7.2f us  %6.2f TB/s\n", name, THREADS, U, grid, best * 1e3,
+         bytes / (best * 1e-3) / 1e12);
+}
+
+template <int THREADS, int ENVS, bool CONTIG, bool NT>
+void run_p(float* obs, int64_t B, unsigned grid, const char* name) {
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_probe_p<THREADS, ENVS, CONTIG, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(a, 0);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_probe_p<THREADS, ENVS, CONTIG, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    best = ms / 20 < best ? ms / 20 : best;
+  }
+  const double bytes = (double)B * PER_ENV * 4;
+  printf("%-44s threads=%4d envs/WG=%3d grid=%6u: %7.2f us  %6.2f TB/s\n", name, THREADS, ENVS, grid, best * 1e3,
+         bytes / (best * 1e-3) / 1e12);
+}
+
 template <int THREADS, int ENVS, int MODE, int U = 1, bool NT = false>
 void run(float* obs, int64_t B, const char* name) {
   const unsigned grid = (unsigned)((B + ENVS - 1) / ENVS);
@@ -112,6 +184,40 @@ int main() {
   run<512, 8, 1, 2, true>(obs, B, "Large 512 lanes 8 envs, gather unroll 2, nt");
   run<512, 8, 2, 1, true>(obs, B, "Large 512 lanes 8 envs, constant stores, nt");
   run<1024, 16, 2, 1, true>(obs, B, "Large 1024 lanes 16 envs, constant stores, nt");
+  run_p<256, 4, true, true>(obs, B, 256 * 8, "persistent contiguous 8/CU, const, nt");
+  run_p<256, 4, false, true>(obs, B, 256 * 8, "persistent interleaved 8/CU, const, nt");
+  run_p<1024, 4, true, true>(obs, B, 256, "persistent contiguous 1x1024/CU, const, nt");
+  run_p<1024, 4, true, true>(obs, B, 512, "persistent contiguous 2x1024/CU, const, nt");
+  run_p<256, 4, true, true>(obs, B, 256 * 4, "persistent contiguous 4/CU, const, nt");
+  run_p<256, 4, true, false>(obs, B, 256 * 8, "persistent contiguous 8/CU, const, plain");
+  run_p<256, 1, false, true>(obs, B, 65536, "1 env per WG (65536 WGs), const, nt");
+  run_p<256, 16, false, true>(obs, B, 4096, "16 envs per WG (4096 WGs), const, nt");
+  run_s<256, 1, true>(obs, B, 2048, "sweep 256 lanes x 2048 WGs, nt");
+  run_s<256, 1, false>(obs, B, 2048, "sweep 256 lanes x 2048 WGs, plain");
+  run_s<256, 4, true>(obs, B, 2048, "sweep 256 lanes x 2048 WGs unroll 4, nt");
+  run_s<256, 4, false>(obs, B, 2048, "sweep 256 lanes x 2048 WGs unroll 4, plain");
+  run_s<256, 1, true>(obs, B, 16384, "sweep 256 lanes x 16384 WGs, nt");
+  run_s<256, 1, true>(obs, B, 148480, "sweep one float4 per lane (no loop), nt");
+  run_s<256, 1, false>(obs, B, 148480, "sweep one float4 per lane (no loop), plain");
+  run_s<1024, 4, false>(obs, B, 512, "sweep 1024 lanes x 512 WGs unroll 4, plain");
+  hipMemset(obs, 0, (size_t)B * PER_ENV * 4);
+  {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+      hipEventRecord(a, 0);
+      for (int i = 0; i < 20; ++i) hipMemsetAsync(obs, i, (size_t)B * PER_ENV * 4, 0);
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      best = ms / 20 < best ? ms / 20 : best;
+    }
+    printf("%-44s %7.2f us  %6.2f TB/s\n", "hipMemsetAsync of the same buffer", best * 1e3,
+           (double)B * PER_ENV * 4 / (best * 1e-3) / 1e12);
+  }
   return 0;
 #endif
   run<256, 16, 0>(obs, B, "k_observe shape, gather");
