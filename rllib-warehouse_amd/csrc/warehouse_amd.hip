@@ -74,6 +74,14 @@ constexpr bool kBiasAddr = false;
 #define WH_OBS_EB0 4
 #endif
 constexpr int kObsEB[4] = {WH_OBS_EB0, 8, 16, 64};   // the observation kernel's instances
+// The widest f32 rows (kObsEB[0]'s: Large) are written in chunks of WH_OBS_CHUNK float4s per workgroup
+// (k_observe's CHUNK form; 0 = each workgroup writes its own envs' rows).  Large-16 sampler step
+// 127 -> 109-112 us, wh_observe 110 -> 100-104 us (profiles/r06_obschunk_ab.txt, r06_obschunk2_ab.txt:
+// 512 / 768 / 1280 / 1536 float4s, plain stores and 2 vs 4 float4s in flight compared).
+#ifndef WH_OBS_CHUNK
+#define WH_OBS_CHUNK 1024
+#endif
+constexpr int kObsChunk = WH_OBS_CHUNK;
 #ifndef WH_FUSE_ROWS_MAX   // rows per env (bytes) up to which the sampler routes fuse step + rows (fuse_rows)
 #define WH_FUSE_ROWS_MAX 4096
 #endif
@@ -2097,11 +2105,10 @@ __constant__ ObsSrc<R, NAM> kObsSrc = make_obs_src<R, NAM>();
 #ifndef WH_ROWS_RU
 #define WH_ROWS_RU 2
 #endif
-template <int NT, int IMG, bool NTS>
+template <int NT, int IMG, bool NTS, int RU = WH_ROWS_RU>
 __device__ __forceinline__ void stream_rows(const uint32_t* lims, const uint32_t* src0, const uint32_t* src1,
                                             const uint8_t* img, f32x4* __restrict__ out4, uint32_t nenv,
                                             uint32_t qe, int tid, uint32_t q0 = 0, uint32_t q1 = ~0u) {
-  constexpr int RU = WH_ROWS_RU;
   const uint32_t magic = 0xFFFFFFFFu / qe + 1u;   // q / qe == umulhi(q, magic) while q * qe < 2^32
   const uint32_t total = nenv * qe < q1 ? nenv * qe : q1;   // float4s [q0, total) of the group
   for (uint32_t q = q0 + tid; q < total; q += RU * NT) {
@@ -2202,7 +2209,12 @@ struct ObsLds {
 // `tile` (32 rows) holds features 16q + 8h + j (j < 8) of row tile*32 + (lane & 31), h = lane >> 5;
 // features L, L+1 are 1.0 (the MLP's bias columns), the rest of the padding 0.  One coalesced
 // 16-byte load per k-step for the MLP instead of scattered f32 rows (and half the bytes).
-template <class C, int OBS_EB>
+// CHUNK > 0 (f32 rows as whole float4s only): workgroup c writes the CHUNK float4s [c * CHUNK,
+// (c + 1) * CHUNK) of the flat rows instead of its own envs' rows, imaging the (at most OBS_EB) envs
+// they belong to -- smaller regions per workgroup, which the write path takes faster (constant
+// stores: 16 KB per workgroup 100 us against 37 KB 113 us for Large-16's 608 MB,
+// profiles/r06_obs_write_probe_chunks.txt).
+template <class C, int OBS_EB, int CHUNK = 0>
 __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ state, int64_t B, int na,
                                                 const uint32_t* __restrict__ tables,
                                                 float* __restrict__ obs, int quads,
@@ -2212,8 +2224,19 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   constexpr int R = C::R, D = C::D, L = C::L, SRCW = ObsLds<C, OBS_EB>::SRCW;
   constexpr int A0 = 1, G0 = 1 + R, P0 = 1 + 3 * R, Q0 = 1 + 5 * R;
   const int tid = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * OBS_EB;
-  const uint32_t nenv = (uint32_t)((B - e0) < OBS_EB ? (B - e0) : OBS_EB);
+  int64_t e0;
+  uint32_t nenv, qlo = 0, qhi = ~0u;
+  if constexpr (CHUNK > 0) {
+    const int64_t qe = (int64_t)na * L / 4;
+    const int64_t qa = (int64_t)blockIdx.x * CHUNK, qb = min(qa + CHUNK, B * qe);
+    e0 = qa / qe;
+    nenv = (uint32_t)((qb - 1) / qe - e0 + 1);   // <= OBS_EB (observe_impl: CHUNK <= (OBS_EB - 1) * qe + 1)
+    qlo = (uint32_t)(qa - e0 * qe);
+    qhi = (uint32_t)(qb - e0 * qe);
+  } else {
+    e0 = (int64_t)blockIdx.x * OBS_EB;
+    nenv = (uint32_t)((B - e0) < OBS_EB ? (B - e0) : OBS_EB);
+  }
   const int el = tid / OBS_PARTS, part = tid % OBS_PARTS;
   const bool mine = (uint32_t)el < nenv;
   const int64_t e = e0 + el;
@@ -2318,8 +2341,11 @@ __global__ __launch_bounds__(BT) void k_observe(const uint32_t* __restrict__ sta
   float* out = obs + e0 * per_env;
   if (quads) {
     // per_env % 4 == 0 and obs 16-byte aligned (checked on the host)
-    stream_rows<BT, ObsLds<C, OBS_EB>::IMG, rows_nt<C>()>(O.lim, O.src[0], O.src[1], &O.img[0][0], reinterpret_cast<f32x4*>(out),
-                                            nenv, per_env >> 2, tid);
+    // (the chunk form: all of a lane's float4s in flight together)
+    constexpr int RU = CHUNK > 0 ? (CHUNK / BT < 1 ? 1 : (CHUNK / BT > 4 ? 4 : CHUNK / BT)) : WH_ROWS_RU;
+    stream_rows<BT, ObsLds<C, OBS_EB>::IMG, rows_nt<C>(), RU>(O.lim, O.src[0], O.src[1], &O.img[0][0],
+                                                              reinterpret_cast<f32x4*>(out), nenv, per_env >> 2, tid,
+                                                              qlo, qhi);
   } else {
     const uint32_t total = nenv * per_env;
     const uint32_t magic = 0xFFFFFFFFu / per_env + 1u;
@@ -2761,6 +2787,7 @@ struct Kernels {
   void (*vsampler[2])(StepParams, float*);  // [ordered]: wh_vector_step's step + rows (external actions)
   void (*reset)(ResetParams);
   void (*observe[4])(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // kObsEB[i] envs per WG
+  void (*observe_chunk)(const uint32_t*, int64_t, int, const uint32_t*, float*, int, uint4*);   // kObsChunk float4s per WG
   int tblw, nv;
 };
 
@@ -2813,6 +2840,7 @@ Kernels make_kernels() {
   k.observe[1] = k_observe<C, kObsEB[1]>;
   k.observe[2] = k_observe<C, kObsEB[2]>;
   k.observe[3] = k_observe<C, kObsEB[3]>;
+  k.observe_chunk = kObsChunk > 0 ? k_observe<C, kObsEB[0], kObsChunk> : nullptr;
   k.tblw = C::TBLW;
   k.nv = C::NV;
   return k;
@@ -3221,6 +3249,12 @@ static int observe_impl(const wh_config* cfg, int64_t B, const uint32_t* state, 
   // grouping of 16 envs = 144 rows does not)
   if (xfrag && (kObsEB[sel] * g.NA) % 32 != 0) sel = 3;
   const int ebx = kObsEB[sel];
+  const int64_t qe = (int64_t)g.NA * (9 * g.R + 1) / 4;
+  if (sel == 0 && !xfrag && quads && k->observe_chunk && kObsChunk <= (ebx - 1) * qe + 1) {
+    hipLaunchKernelGGL(k->observe_chunk, dim3((unsigned)((B * qe + kObsChunk - 1) / kObsChunk)), dim3(BT), 0,
+                       (hipStream_t)stream, state, B, g.NA, tab, obs, quads, static_cast<uint4*>(xfrag));
+    return hip_err(hipGetLastError());
+  }
   hipLaunchKernelGGL(k->observe[sel], dim3((unsigned)((B + ebx - 1) / ebx)), dim3(BT), 0,
                      (hipStream_t)stream, state, B, g.NA, tab, obs, quads, static_cast<uint4*>(xfrag));
   return hip_err(hipGetLastError());

@@ -31,6 +31,10 @@ for variant, na in SHAPES:
     obs = env.observe()
     xf = env.observe_x()
     torch.cuda.synchronize()
+    o = env.observe()
+    w = (torch.arange(o.numel(), device=o.device, dtype=torch.float64) % 9973 + 1).view(o.shape)
+    print(f"{variant:6s} na={na:2d} observe rows fingerprint {float((o.double() * w).sum()):.1f} "
+          f"(sum {float(o.double().sum()):.1f})", flush=True)
     us = timed(env.observe)
     nbytes = obs.numel() * 4 + env.state.numel() * 4
     print(f"{variant:6s} na={na:2d} observe   {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #ifdef PROBE_LARGE   // Large-16 rows: 16 x 145 floats per env (round 6: what bounds k_observe<Large>?)
 constexpr int NA = 16, L = 145, IMG = 148, PER_ENV = NA * L, QE = PER_ENV / 4;   // 580 float4 per env
@@ -126,6 +127,41 @@ void run_s(float* obs, int64_t B, unsigned grid, const char* name) {
          bytes / (best * 1e-3) / 1e12);
 }
 
+// No loop: workgroup w writes the U * THREADS float4s [w * U * THREADS, (w + 1) * U * THREADS), U
+// stores per lane issued back to back, workgroups in dispatch order (the stores in flight form one
+// moving window of about resident-workgroups x U x 4 KB).
+template <int THREADS, int U, bool NT>
+__global__ __launch_bounds__(THREADS) void k_chunk(float* __restrict__ obs, int64_t n4) {
+  f32x4* out4 = reinterpret_cast<f32x4*>(obs);
+  const int64_t q0 = (int64_t)blockIdx.x * (U * THREADS) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (q0 + u * THREADS < n4) st<NT>(&out4[q0 + u * THREADS], (f32x4){1.0f, 2.0f, 3.0f, 4.0f});
+}
+
+template <int THREADS, int U, bool NT>
+void run_c(float* obs, int64_t B, const char* name) {
+  const int64_t n4 = B * (int64_t)QE;
+  const unsigned grid = (unsigned)((n4 + U * THREADS - 1) / (U * THREADS));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_chunk<THREADS, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, n4);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(a, 0);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_chunk<THREADS, U, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, n4);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    best = ms / 20 < best ? ms / 20 : best;
+  }
+  const double bytes = (double)B * PER_ENV * 4;
+  printf("%-44s threads=%4d stores/lane=%d grid=%6u: %7.2f us  %6.2f TB/s\n", name, THREADS, U, grid, best * 1e3,
+         bytes / (best * 1e-3) / 1e12);
+}
+
 template <int THREADS, int ENVS, bool CONTIG, bool NT>
 void run_p(float* obs, int64_t B, unsigned grid, const char* name) {
   for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_probe_p<THREADS, ENVS, CONTIG, NT>), dim3(grid), dim3(THREADS), 0, 0, obs, B);
@@ -174,6 +210,18 @@ int main() {
   float* obs;
   hipMalloc(&obs, (size_t)B * PER_ENV * 4);
 #ifdef PROBE_LARGE
+  if (getenv("PROBE_CHUNKS")) {
+    run_c<256, 1, true>(obs, B, "chunk 4 KB per WG, nt");
+    run_c<256, 1, false>(obs, B, "chunk 4 KB per WG, plain");
+    run_c<256, 2, true>(obs, B, "chunk 8 KB per WG, nt");
+    run_c<256, 4, true>(obs, B, "chunk 16 KB per WG, nt");
+    run_c<256, 4, false>(obs, B, "chunk 16 KB per WG, plain");
+    run_c<256, 8, true>(obs, B, "chunk 32 KB per WG, nt");
+    run_c<256, 9, true>(obs, B, "chunk 36 KB per WG, nt");
+    run_c<512, 4, true>(obs, B, "chunk 32 KB per 512-lane WG, nt");
+    run_c<1024, 2, true>(obs, B, "chunk 32 KB per 1024-lane WG, nt");
+    return 0;
+  }
   run<256, 4, 0, 1, true>(obs, B, "Large k_observe shape (4 envs), gather, nt");
   run<256, 4, 1, 2, true>(obs, B, "Large 4 envs, gather unroll 2, nt");
   run<256, 4, 2, 1, true>(obs, B, "Large 4 envs, constant stores, nt");
