@@ -268,6 +268,16 @@ int main() {
   }
   return 0;
 #endif
+  if (getenv("PROBE_CHUNKS")) {   // Medium-8 rows (172 MB): chunked regions vs the fused launch's 672 KB ones
+    for (int pass = 0; pass < 2; ++pass) {
+      run<512, 256, 2>(obs, B, "fused 512 lanes 256 envs (672 KB/WG), constant");
+      run<256, 16, 2>(obs, B, "k_observe shape 16 envs (42 KB/WG), constant");
+      run_c<256, 1, false>(obs, B, "chunk 4 KB per WG, plain");
+      run_c<256, 4, false>(obs, B, "chunk 16 KB per WG, plain");
+      run_c<256, 8, false>(obs, B, "chunk 32 KB per WG, plain");
+    }
+    return 0;
+  }
   run<256, 16, 0>(obs, B, "k_observe shape, gather");
   run<256, 16, 2>(obs, B, "k_observe shape, constant stores");
   run<256, 64, 0>(obs, B, "256 lanes 64 envs, gather");
