@@ -97,6 +97,33 @@ def test_vector_step_autoreset_obs_stats_vs_oracle(wh, variant, na, train):
 
 
 
+@pytest.mark.parametrize("na,B", [(16, 7), (12, 333), (16, 1000), (8, 129)])
+def test_chunked_large_rows_vs_oracle(wh, na, B):
+    """Large f32 rows are written in 1,024-float4 chunks per workgroup (k_observe's CHUNK form), each
+    imaging the envs its chunk touches: chunks that start mid-env and span three (16 agents) or four
+    (12 agents) envs, a ragged last chunk, a batch smaller than one chunk; 8 agents (rows of 290
+    float4s: more envs per chunk than the instance images) takes the per-group form.  Rows vs the
+    oracle after resets and every external-action step."""
+    L = oc.layout_for("large")
+    seed = 5
+    venv = wh.vector.WarehouseVectorEnv("large", B, na, train=False, seed=seed)
+    obs = venv.vector_reset().cpu().numpy()
+    S = ob.BState.zeros(L, B, na)
+    ids = np.arange(B)
+    ob.reset(L, S, ob.PhiloxDraws(seed, ids))
+    np.testing.assert_array_equal(obs, ob.observe(L, S))
+    rng = np.random.RandomState(2)
+    d = ob.PhiloxDraws(seed, ids)
+    for s in range(30):
+        acts = rng.randint(0, 9, size=(B, na)).astype(np.int32)
+        obs, rew, done, _ = venv.vector_step(acts)
+        orew, odone, _, _ = ob.step(L, S, acts, d)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orew, err_msg=f"step {s}")
+        if odone.any():
+            ob.reset(L, S, d, mask=odone)
+        np.testing.assert_array_equal(obs.cpu().numpy(), ob.observe(L, S), err_msg=f"obs step {s}")
+
+
 @pytest.mark.parametrize("variant,na,train,p", [("medium", 9, True, 0.1), ("medium", 8, False, 0.0)])
 def test_rollout_episode_stats_vs_oracle(wh, variant, na, train, p):
     """wh_rollout with wh_episode_stats over two launches (the running returns persist between
