@@ -44,7 +44,11 @@ except ImportError:
 
             def contains(self, x):
                 x = np.asarray(x)
-                return x.shape == self.shape and bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
+                if x.shape != self.shape:
+                    return False
+                if x.size and np.isscalar(self.low) and np.isscalar(self.high):   # two reductions, no temporaries
+                    return bool(x.min() >= self.low) and bool(x.max() <= self.high)
+                return bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
 
         class MultiBinary(Space):
             def __init__(self, n):
@@ -53,7 +57,11 @@ except ImportError:
 
             def contains(self, x):
                 x = np.asarray(x)
-                return x.shape == (self.n,) and bool(np.all((x == 0) | (x == 1)))
+                if x.shape != (self.n,):
+                    return False
+                if x.size and x.dtype.kind in "biu":                 # integers: {0, 1} <=> 0 <= x <= 1
+                    return bool(x.min() >= 0) and bool(x.max() <= 1)
+                return bool(np.all((x == 0) | (x == 1)))
 
         class Dict(Space):
             def __init__(self, spaces):
