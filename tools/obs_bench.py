@@ -39,6 +39,9 @@ for variant, na in SHAPES:
     nbytes = obs.numel() * 4 + env.state.numel() * 4
     print(f"{variant:6s} na={na:2d} observe   {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "
           f"(rows {obs.numel() * 4 / 1e6:.1f} MB + state {env.state.numel() * 4 / 1e6:.1f} MB)", flush=True)
+    xb = env.observe_x().view(-1).to(torch.int64)
+    print(f"{variant:6s} na={na:2d} observe_x operand fingerprint "
+          f"{int(((xb & 0xFF) * (torch.arange(xb.numel(), device=xb.device) % 9973 + 1)).sum())}", flush=True)
     us = timed(env.observe_x)
     nbytes = xf.numel() + env.state.numel() * 4
     print(f"{variant:6s} na={na:2d} observe_x {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "
