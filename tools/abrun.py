@@ -16,6 +16,7 @@ SPEC.json:
         {"name": "r04", "rev": "f6d71ed"},            # the library at a git revision (its own Makefile)
         {"name": "r04x", "rev": "f6d71ed", "flags": "-DWH_Y"},
         {"name": "l16", "flags": "-DWH_ONLY_LARGE16", "commands": ["..."]},   # own commands
+        {"name": "ilp", "flags": "-DWH_ONLY_MEDIUM8", "sched": "-mllvm -amdgpu-sched-strategy=max-ilp"},   # scheduler
         {"name": "tree_x", "lib": "tree", "env": {"WH_SAMPLER_UNFUSED": "1"}}],   # same library, env
      "commands": ["python tools/step_probe.py --steps 200 --launches 6",
                   "python tools/step_probe.py --variant large --agents 16 --steps 20 --launches 8"],
@@ -56,7 +57,8 @@ def recipe(v):
         return (f"git archive {v['rev']} rllib-warehouse_amd/csrc include | tar -x -C build/rev_{v['name']} && "
                 f"make -C build/rev_{v['name']}/rllib-warehouse_amd/csrc OUT=$PWD/{os.path.relpath(lib_path(v), ROOT)} "
                 + (f"EXTRA='{v['flags']}'" if v.get("flags") else ""))
-    return f"bash tools/build_variant.sh {v['name']} {v.get('flags', '')}".strip()
+    pre = f"SCHED='{v['sched']}' " if v.get("sched") else ""
+    return f"{pre}bash tools/build_variant.sh {v['name']} {v.get('flags', '')}".strip()
 
 
 def build(spec):
@@ -81,8 +83,9 @@ def build(spec):
                 cmd.append(f"EXTRA={v['flags']}")
             subprocess.run(cmd, check=True)
         else:
+            env = dict(os.environ, SCHED=v["sched"]) if v.get("sched") else None   # the step object's scheduler flags
             subprocess.run(["bash", os.path.join(ROOT, "tools", "build_variant.sh"), v["name"]]
-                           + shlex.split(v.get("flags", "")), check=True)
+                           + shlex.split(v.get("flags", "")), check=True, env=env)
         print(f"built {v['name']}: {lib_path(v)}", flush=True)
 
 

@@ -5,4 +5,8 @@
 cd "$(dirname "$0")/../rllib-warehouse_amd/csrc" || exit 2
 NAME=$1; shift
 mkdir -p ../../build_ab
-make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*" lib
+if [ -n "$SCHED" ]; then   # another scheduler setting for the step object (abrun "sched")
+  make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*" SCHED_warehouse_amd="$SCHED" lib
+else
+  make -s -j2 OUT=../../build_ab/$NAME.so OBJDIR=../../build/obj_$NAME EXTRA="$*" lib
+fi
