@@ -124,6 +124,23 @@ def test_chunked_large_rows_vs_oracle(wh, na, B):
         np.testing.assert_array_equal(obs.cpu().numpy(), ob.observe(L, S), err_msg=f"obs step {s}")
 
 
+def test_large_rows_unaligned_output_equal_the_chunked_rows(wh):
+    """An f32 row buffer that is not 16-byte aligned cannot take the chunked float4 writer: the
+    per-group scalar form writes it, with the same rows."""
+    import torch
+    from warehouse import _native as nat
+
+    env = wh.BatchedWarehouse("large", 300, 16, seed=4)
+    env.reset()
+    env.rollout(17, "greedy", 0.0)
+    ref = env.observe().clone()
+    buf = torch.zeros(ref.numel() + 1, device=env.device)
+    nat.check(nat.lib().wh_observe(env._cfgp, env.B, env.state.data_ptr(), buf.data_ptr() + 4, env.stream),
+              "wh_observe")
+    torch.cuda.synchronize()
+    assert torch.equal(buf[1:].view_as(ref), ref)
+
+
 @pytest.mark.parametrize("variant,na,train,p", [("medium", 9, True, 0.1), ("medium", 8, False, 0.0)])
 def test_rollout_episode_stats_vs_oracle(wh, variant, na, train, p):
     """wh_rollout with wh_episode_stats over two launches (the running returns persist between
